@@ -1,0 +1,174 @@
+"""Headline benchmark: fitness evaluations per second (hcv + scv + feasibility +
+penalty, Solution.cpp:63-170) of a device-resident population of 65,536
+individuals on the 400-event medium01-size instance, per GPU (weak scaling:
+one independent population shard per rank, no data-path collective).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+A step is one tt_eval over the rank's whole population. Rank 0 prints one JSON
+line (BASELINE.json metric) with the dominant kernel's roofline and, at N=1, a
+CPU baseline: the reference's own computeFeasibility/Hcv/Scv (oracle/_ref,
+OpenMP over individuals) timed on a bounded sample of the same population.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+REPO = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "timetabling-ga-mpi-openmp_amd"))
+sys.path.insert(0, str(REPO / "tests"))
+
+METRIC = json.loads((REPO / "BASELINE.json").read_text())["metric"]
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+POP_PER_GPU = 65536
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--pop", type=int, default=POP_PER_GPU)
+    ap.add_argument("--config", default="med", choices=["sm", "med", "lg", "syn"])
+    ap.add_argument("--variant", type=int, default=0, help="tt_eval kernel: 0 auto, 1 lanes, 2 block")
+    ap.add_argument("--cpu-sample", type=int, default=16384, help="individuals in the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(inst, slot_np, room_np, gpu_out):
+    """The reference's evaluation (oracle/_ref) or, without it, the oracle port."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    from oracle_lib import REF_PATH, oracle, ref
+    n = slot_np.shape[0]
+    hcv = np.zeros(n, np.int32); scv = np.zeros(n, np.int32)
+    feas = np.zeros(n, np.uint8); pen = np.zeros(n, np.int32)
+    R = ref()
+    if R is not None:
+        h = R.problem(inst)
+        fn = R.lib.ref_eval_timed
+        fn.restype = ctypes.c_double
+        fn.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 2 + [ctypes.c_void_p] * 4
+        P_ = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        secs = fn(h.h, P_(slot_np), P_(room_np), n, threads, P_(hcv), P_(scv), P_(feas), P_(pen))
+        kind, cores = "reference", threads
+    else:
+        o = oracle().problem(inst)
+        t0 = time.perf_counter()
+        hcv, scv, feas, pen = o.eval(slot_np, room_np)
+        secs = time.perf_counter() - t0
+        kind, cores = "port", 1
+    agree = all(np.array_equal(a, b[:n]) for a, b in zip((hcv, scv, feas, pen), gpu_out))
+    return {"value": n / secs, "unit": "evals/s", "cores": cores, "kind": kind,
+            "sample": f"{n} individuals of the same population, computeFeasibility+computeHcv+computeScv+penalty, "
+                      f"OpenMP dynamic over individuals, {secs:.2f} s", "matches_gpu": bool(agree)}
+
+
+def pmc_traffic(workload_key):
+    f = REPO / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        return d.get(workload_key)
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import ttga
+    from ttga import native
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    inst = ttga.config_instance(args.config)
+    dp = native.DeviceProblem(inst, device=local)
+    P, E = args.pop, inst.E
+    # synthetic population: RandomInitialSolution per individual (seed base 12345 + global index),
+    # canonical rooms from the matcher; setup, not timed
+    seeds = torch.from_numpy(ttga.population_seeds(12345 + rank * P, P)).to(dev)
+    slot = torch.empty((P, E), dtype=torch.uint8, device=dev)
+    room = torch.empty_like(slot)
+    dp.random_init(seeds, slot, room)
+    out = (torch.empty(P, dtype=torch.int32, device=dev), torch.empty(P, dtype=torch.int32, device=dev),
+           torch.empty(P, dtype=torch.uint8, device=dev), torch.empty(P, dtype=torch.int32, device=dev))
+    torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        dp.eval(slot, room, variant=args.variant, out=out)
+    torch.cuda.synchronize(dev)
+
+    stream = torch.cuda.current_stream(dev)      # tt_eval launches its one kernel on this stream
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        dp.eval(slot, room, variant=args.variant, out=out)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+
+    if rank == 0:
+        total = P * world * args.steps
+        value = total / wall_max
+        bytes_per_eval = 2 * E + 13                     # u8 slot+room in; i32 hcv,scv,penalty + u8 feasible out
+        achieved = bytes_per_eval * P / (kernel_ms * 1e-3) / 1e9
+        variant = args.variant or (1 if E <= 1024 else 2)
+        wkey = f"{args.config}_P{P}_v{variant}"
+        tr = pmc_traffic(wkey)
+        line = {
+            "metric": METRIC, "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": wall_max / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "i32", "data": "synthetic",
+            "config": {"workload": f"{args.config} instance E={E} R={inst.R} F={inst.F} S={inst.S} (seeded synthetic, "
+                                   f"medium01-size), population {P} per GPU, one tt_eval (hcv+scv+feasible+penalty) "
+                                   f"per step", "pop_per_gpu": P, "global_pop": P * world,
+                       "kernel": "eval_lanes" if variant == 1 else "eval_block",
+                       "parallelism": f"dp{world} (independent population shards)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": tr,
+                         "kernel_ms": kernel_ms, "bytes_per_eval": bytes_per_eval},
+        }
+        if world == 1 and not args.no_cpu:
+            n = min(args.cpu_sample, P)
+            s_np, r_np = slot[:n].cpu().numpy(), room[:n].cpu().numpy()
+            gpu_out = [o[:n].cpu().numpy() for o in out]
+            line["cpu_baseline"] = cpu_baseline(inst, s_np, r_np, gpu_out)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,114 @@
+/* ttga.h — C-ABI of the MI355X-native evaluation-and-evolution engine for the
+ * Rossi-Doria/Paechter course-timetabling GA (drop-in for the hot path of
+ * nelilepo/timetabling-ga-mpi-openmp).
+ *
+ * The reference has no FFI layer: its boundary is the C++ class API of
+ * Problem (Problem.h:32-51) and Solution (Solution.h:33-83), called only from
+ * ga.cpp. Each entry point below replaces one of those calls, batched over a
+ * population of P individuals that lives in device memory (HBM):
+ *
+ *   population layout (caller-owned device buffers, individual-major):
+ *     slot[P][E]  uint8  timeslot of each event, 0..44   (Solution::sln[e].first)
+ *     room[P][E]  uint8  room of each event, 0..R-1      (Solution::sln[e].second)
+ *     rng[P]      int64  one Park-Miller state per individual (Random::seed)
+ *
+ * Conventions: every function returns TT_OK (0) or a TT_ERR_* code and never
+ * throws; tt_last_error() gives a message for the calling thread. Every
+ * device-side call is asynchronous on the caller's stream (a hipStream_t
+ * passed as void*; NULL = default stream). One tt_problem may be used by
+ * several host threads on different streams. Nothing here falls back to the
+ * CPU: without a usable gfx950 device the calls fail with TT_ERR_DEVICE.
+ *
+ * Limits: 1 <= E <= 65535, 1 <= R <= 64, S >= 0, F >= 0; at most 256 events
+ * share one timeslot inside tt_assign_rooms/tt_local_search (beyond that the
+ * affected rooms are written as 255 and tt_device_status() reports it).
+ */
+#ifndef TTGA_H
+#define TTGA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TT_OK 0
+#define TT_ERR_INVALID 1   /* bad argument (null pointer, size, non-binary matrix) */
+#define TT_ERR_DEVICE 2    /* HIP runtime/device failure */
+#define TT_ERR_LIMIT 3     /* instance outside the documented limits */
+
+#define TT_NUM_SLOTS 45    /* 5 days x 9 slots, Solution.cpp:52,57 */
+
+typedef struct tt_problem tt_problem;
+
+/* Replaces Problem::Problem(istream&) (Problem.cpp:3-96) and the MPI problem
+ * broadcast (ga.cpp:417-426): takes the parsed .tim matrices, derives
+ * studentNumber, eventCorrelations and possibleRooms exactly as
+ * Problem.cpp:86-148, and uploads the device image to `device`.
+ *   room_size[R], student_events[S*E] (row-major, 0/1), room_features[R*F],
+ *   event_features[E*F] (0/1). */
+int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, const int32_t* student_events,
+                      const int32_t* room_features, const int32_t* event_features, int device,
+                      tt_problem** out);
+
+/* Problem::~Problem (Problem.cpp:114-120). */
+int tt_problem_destroy(tt_problem* p);
+
+/* dims[0..3] = E, R, F, S (Problem.h:35-38). */
+int tt_problem_dims(const tt_problem* p, int32_t* dims);
+
+/* Host copies of the derived matrices (Problem.h:39,42,46); any pointer may be NULL.
+ *   student_number[E], corr[E*E], possible[E*R]. */
+int tt_problem_derived(const tt_problem* p, int32_t* student_number, int32_t* corr, int32_t* possible);
+
+/* Batched Solution::computeFeasibility / computeHcv / computeScv /
+ * computePenalty (Solution.cpp:63-170; penalty = scv if feasible else
+ * 1000000 + hcv). Outputs are device buffers of length P. hcv and scv are
+ * always both computed. An individual with slot >= 45 or room >= R is
+ * reported as hcv = scv = penalty = -1, feasible = 0. */
+int tt_eval(const tt_problem* p, const uint8_t* slot, const uint8_t* room, int P, int32_t* hcv, int32_t* scv,
+            uint8_t* feasible, int32_t* penalty, void* stream);
+
+/* tt_eval with an explicit kernel choice: 0 = automatic, 1 = lane-per-individual
+ * (E <= 1024), 2 = workgroup-per-individual (any E). For tests and profiling. */
+int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const uint8_t* room, int P, int32_t* hcv,
+                    int32_t* scv, uint8_t* feasible, int32_t* penalty, int variant, void* stream);
+
+/* Solution::assignRooms (Solution.cpp:772-891) on every non-empty timeslot in
+ * ascending order, events of a slot in ascending index: the max-cardinality
+ * matching found by the reference's priority-first-search augmentation,
+ * unmatched events sent to the least-busy possible room (busy[] starting at
+ * 0). Writes room[P][E]. */
+int tt_assign_rooms(const tt_problem* p, const uint8_t* slot, uint8_t* room, int P, void* stream);
+
+/* Solution::RandomInitialSolution (Solution.cpp:48-61) per individual, each
+ * with its own Random stream rng[i] (advanced in place by E draws). */
+int tt_random_init(const tt_problem* p, int64_t* rng, uint8_t* slot, uint8_t* room, int P, void* stream);
+
+/* Solution::crossover (Solution.cpp:893-910) into a fresh child: per event,
+ * next() < 0.5 takes parent 1's slot else parent 2's, then assignRooms.
+ * parent1/parent2/child are [P][E] slot arrays; rng advanced by E draws. */
+int tt_crossover(const tt_problem* p, const uint8_t* slot1, const uint8_t* slot2, int64_t* rng, uint8_t* slot,
+                 uint8_t* room, int P, void* stream);
+
+/* Solution::mutation -> randomMove (Solution.cpp:441-469,912-914), in place. */
+int tt_mutation(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P, void* stream);
+
+/* Solution::localSearch(maxSteps, LS_limit, p1, p2, p3) (Solution.cpp:471-769)
+ * per individual with its own Random stream; in place. The LS_limit wall-clock
+ * bound (999999 s by default, never binding) is not modelled. */
+int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P, int max_steps,
+                    double p1, double p2, double p3, void* stream);
+
+/* Device-side status word of the problem handle (0 = fine; bit 0 = a slot
+ * exceeded 256 events in a matching). Synchronises the device. */
+int tt_device_status(const tt_problem* p, int32_t* status);
+
+const char* tt_last_error(void);
+int tt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TTGA_H */

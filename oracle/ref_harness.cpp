@@ -1,0 +1,221 @@
+// ref_harness — TEST INFRASTRUCTURE ONLY.
+//
+// A thin extern "C" shim over the reference's OWN Problem / Solution / Random
+// objects (nelilepo/timetabling-ga-mpi-openmp, compiled unmodified from
+// /root/reference by oracle/Makefile into oracle/_ref/libttref.so). Used to
+// (1) generate the golden vectors committed under tests/golden/ and
+// (2) time the reference's evaluation functions as bench.py's CPU baseline.
+//
+// Reference F1 (uninitialised busy[] VLA, Solution.cpp:778) is neutralised
+// WITHOUT editing the sources: the Makefile compiles them with clang's
+// -ftrivial-auto-var-init=zero, which zero-fills that VLA.
+//
+// Written in C++98 (the reference's Random.h needs gnu++98).
+#include <sstream>
+#include <vector>
+#include <sys/time.h>
+#include <omp.h>
+
+#include "Problem.h"
+#include "Solution.h"
+#include "Random.h"
+
+typedef unsigned char u8;
+
+static void load_solution(Solution* s, const u8* slot, const u8* room, int E) {
+    // deserializeSolution-style construction (ga.cpp:344-368): sln pairs, then
+    // timeslot_events built by ascending event index.
+    for (int e = 0; e < E; e++) {
+        s->sln[e].first = slot[e];
+        s->sln[e].second = room ? room[e] : -1;
+    }
+    for (int e = 0; e < E; e++) s->timeslot_events[slot[e]].push_back(e);
+}
+
+static void store_solution(const Solution* s, u8* slot, u8* room, int E) {
+    for (int e = 0; e < E; e++) {
+        if (slot) slot[e] = (u8)s->sln[e].first;
+        if (room) room[e] = (u8)s->sln[e].second;
+    }
+}
+
+extern "C" {
+
+// Builds a .tim text image and parses it with the reference's Problem(istream&).
+void* ref_problem_create(int E, int R, int F, int S, const int* room_size, const int* A,
+                         const int* room_feat, const int* event_feat) {
+    std::ostringstream os;
+    os << E << " " << R << " " << F << " " << S << "\n";
+    for (int r = 0; r < R; r++) os << room_size[r] << "\n";
+    for (long i = 0; i < (long)S * E; i++) os << A[i] << "\n";
+    for (long i = 0; i < (long)R * F; i++) os << room_feat[i] << "\n";
+    for (long i = 0; i < (long)E * F; i++) os << event_feat[i] << "\n";
+    std::istringstream is(os.str());
+    return new Problem(is);
+}
+
+void* ref_problem_from_tim(const char* path) {
+    std::ifstream is(path);
+    return new Problem(is);
+}
+
+void ref_problem_destroy(void* p) { delete (Problem*)p; }
+
+void ref_problem_dims(const void* p, int* dims) {
+    const Problem* P = (const Problem*)p;
+    dims[0] = P->n_of_events; dims[1] = P->n_of_rooms; dims[2] = P->n_of_features; dims[3] = P->n_of_students;
+}
+
+void ref_problem_derived(const void* p, int* student_number, int* corr, int* possible) {
+    const Problem* P = (const Problem*)p;
+    const int E = P->n_of_events, R = P->n_of_rooms;
+    for (int i = 0; i < E; i++) student_number[i] = P->studentNumber[i];
+    for (int i = 0; i < E; i++)
+        for (int j = 0; j < E; j++) corr[(long)i * E + j] = P->eventCorrelations[i][j];
+    for (int i = 0; i < E; i++)
+        for (int j = 0; j < R; j++) possible[(long)i * R + j] = P->possibleRooms[i][j];
+}
+
+void ref_problem_matrices(const void* p, int* room_size, int* A, int* room_feat, int* event_feat) {
+    const Problem* P = (const Problem*)p;
+    const int E = P->n_of_events, R = P->n_of_rooms, F = P->n_of_features, S = P->n_of_students;
+    for (int r = 0; r < R; r++) room_size[r] = P->roomSize[r];
+    for (int s = 0; s < S; s++)
+        for (int e = 0; e < E; e++) A[(long)s * E + e] = P->student_events[s][e];
+    for (int r = 0; r < R; r++)
+        for (int f = 0; f < F; f++) room_feat[(long)r * F + f] = P->room_features[r][f];
+    for (int e = 0; e < E; e++)
+        for (int f = 0; f < F; f++) event_feat[(long)e * F + f] = P->event_features[e][f];
+}
+
+void ref_rand(long seed, int n, double* out, long* final_state) {
+    Random r(0);
+    r.seed = seed;
+    for (int i = 0; i < n; i++) out[i] = r.next();
+    *final_state = r.seed;
+}
+
+// computeFeasibility / computeHcv / computeScv / computePenalty per individual.
+void ref_eval(void* p, const u8* slot, const u8* room, int np, int* hcv, int* scv, u8* feasible,
+              int* penalty) {
+    Problem* P = (Problem*)p;
+    const int E = P->n_of_events;
+    Random r(1);
+    for (int i = 0; i < np; i++) {
+        Solution s(P, &r);
+        load_solution(&s, slot + (long)i * E, room + (long)i * E, E);
+        feasible[i] = s.computeFeasibility() ? 1 : 0;
+        hcv[i] = s.computeHcv();
+        scv[i] = s.computeScv();
+        penalty[i] = s.computePenalty();
+    }
+}
+
+// CPU baseline: the same evaluation, OpenMP over individuals. Solutions are
+// built before the clock starts; the timed region is exactly
+// computeFeasibility + computeHcv + computeScv + penalty.
+// Returns seconds.
+double ref_eval_timed(void* p, const u8* slot, const u8* room, int np, int threads, int* hcv, int* scv,
+                      u8* feasible, int* penalty) {
+    Problem* P = (Problem*)p;
+    const int E = P->n_of_events;
+    Random r(1);
+    std::vector<Solution*> pop(np);
+    for (int i = 0; i < np; i++) {
+        pop[i] = new Solution(P, &r);
+        load_solution(pop[i], slot + (long)i * E, room + (long)i * E, E);
+        for (int t = 0; t < 45; t++) pop[i]->timeslot_events[t];   // materialise all map keys
+    }
+    omp_set_num_threads(threads);
+    struct timeval t0, t1;
+    gettimeofday(&t0, 0);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int i = 0; i < np; i++) {
+        Solution* s = pop[i];
+        bool f = s->computeFeasibility();
+        int h = s->computeHcv();
+        int c = s->computeScv();
+        hcv[i] = h;
+        scv[i] = c;
+        feasible[i] = f ? 1 : 0;
+        penalty[i] = f ? c : 1000000 + h;
+    }
+    gettimeofday(&t1, 0);
+    for (int i = 0; i < np; i++) delete pop[i];
+    return (t1.tv_sec - t0.tv_sec) + 1e-6 * (t1.tv_usec - t0.tv_usec);
+}
+
+// assignRooms on every non-empty slot, ascending t.
+void ref_assign_rooms(void* p, const u8* slot, u8* room, int np) {
+    Problem* P = (Problem*)p;
+    const int E = P->n_of_events;
+    Random r(1);
+    for (int i = 0; i < np; i++) {
+        Solution s(P, &r);
+        load_solution(&s, slot + (long)i * E, 0, E);
+        for (int t = 0; t < 45; t++)
+            if ((int)s.timeslot_events[t].size()) s.assignRooms(t);
+        store_solution(&s, 0, room + (long)i * E, E);
+    }
+}
+
+void ref_random_init(void* p, long* rng, u8* slot, u8* room, int np) {
+    Problem* P = (Problem*)p;
+    const int E = P->n_of_events;
+    for (int i = 0; i < np; i++) {
+        Random r(0);
+        r.seed = rng[i];
+        Solution s(P, &r);
+        s.RandomInitialSolution();
+        store_solution(&s, slot + (long)i * E, room + (long)i * E, E);
+        rng[i] = r.seed;
+    }
+}
+
+void ref_local_search(void* p, u8* slot, u8* room, long* rng, int np, int max_steps, double p1, double p2,
+                      double p3) {
+    Problem* P = (Problem*)p;
+    const int E = P->n_of_events;
+    for (int i = 0; i < np; i++) {
+        Random r(0);
+        r.seed = rng[i];
+        Solution s(P, &r);
+        load_solution(&s, slot + (long)i * E, room + (long)i * E, E);
+        s.localSearch(max_steps, 999999, p1, p2, p3);
+        store_solution(&s, slot + (long)i * E, room + (long)i * E, E);
+        rng[i] = r.seed;
+    }
+}
+
+// Crossover into a FRESH child (no prior RandomInitialSolution), i.e. the
+// reference's crossover without the F2 stale-list defect.
+void ref_crossover(void* p, const u8* slot1, const u8* slot2, long* rng, u8* slot, u8* room, int np) {
+    Problem* P = (Problem*)p;
+    const int E = P->n_of_events;
+    for (int i = 0; i < np; i++) {
+        Random r(0);
+        r.seed = rng[i];
+        Solution a(P, &r), b(P, &r), c(P, &r);
+        load_solution(&a, slot1 + (long)i * E, 0, E);
+        load_solution(&b, slot2 + (long)i * E, 0, E);
+        c.crossover(&a, &b);
+        store_solution(&c, slot + (long)i * E, room + (long)i * E, E);
+        rng[i] = r.seed;
+    }
+}
+
+void ref_mutation(void* p, u8* slot, u8* room, long* rng, int np) {
+    Problem* P = (Problem*)p;
+    const int E = P->n_of_events;
+    for (int i = 0; i < np; i++) {
+        Random r(0);
+        r.seed = rng[i];
+        Solution s(P, &r);
+        load_solution(&s, slot + (long)i * E, room + (long)i * E, E);
+        s.mutation();
+        store_solution(&s, slot + (long)i * E, room + (long)i * E, E);
+        rng[i] = r.seed;
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,143 @@
+"""ctypes access to the CPU checkers — TEST INFRASTRUCTURE ONLY.
+
+* `Oracle`  -> oracle/libttoracle.so, the clean-room CPU restatement
+* `Ref`     -> oracle/_ref/libttref.so, the reference's own Problem/Solution
+              objects compiled unmodified (present only where /root/reference
+              was available at build time; it travels with the snapshot)
+
+Both expose the same batched API over numpy arrays so tests can run either.
+"""
+from __future__ import annotations
+
+import ctypes
+import pathlib
+
+import numpy as np
+
+REPO = pathlib.Path(__file__).resolve().parent.parent
+ORACLE_PATH = REPO / "oracle" / "libttoracle.so"
+REF_PATH = REPO / "oracle" / "_ref" / "libttref.so"
+
+_vp = ctypes.c_void_p
+
+
+def _p(a):
+    return a.ctypes.data_as(_vp)
+
+
+class _Checker:
+    prefix = ""
+
+    def __init__(self, path):
+        self.lib = ctypes.CDLL(str(path))
+        pre = self.prefix
+        L = self.lib
+        i32, dbl, lng = ctypes.c_int, ctypes.c_double, ctypes.c_long
+        getattr(L, pre + "problem_create").restype = _vp
+        getattr(L, pre + "problem_create").argtypes = [i32, i32, i32, i32, _vp, _vp, _vp, _vp]
+        getattr(L, pre + "problem_destroy").argtypes = [_vp]
+        getattr(L, pre + "problem_derived").argtypes = [_vp, _vp, _vp, _vp]
+        getattr(L, pre + "rand").argtypes = [lng, i32, _vp, _vp]
+        getattr(L, pre + "eval").argtypes = [_vp, _vp, _vp, i32, _vp, _vp, _vp, _vp]
+        getattr(L, pre + "assign_rooms").argtypes = [_vp, _vp, _vp, i32]
+        getattr(L, pre + "random_init").argtypes = [_vp, _vp, _vp, _vp, i32]
+        getattr(L, pre + "local_search").argtypes = [_vp, _vp, _vp, _vp, i32, i32, dbl, dbl, dbl]
+        getattr(L, pre + "crossover").argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, i32]
+        getattr(L, pre + "mutation").argtypes = [_vp, _vp, _vp, _vp, i32]
+
+    def _f(self, name):
+        return getattr(self.lib, self.prefix + name)
+
+    def problem(self, inst):
+        h = self._f("problem_create")(inst.E, inst.R, inst.F, inst.S, _p(inst.room_size), _p(inst.student_events),
+                                      _p(inst.room_features), _p(inst.event_features))
+        return _Handle(self, h, inst)
+
+    def rand(self, seed: int, n: int):
+        out = np.zeros(n, np.float64)
+        st = ctypes.c_long(0)
+        self._f("rand")(int(seed), n, _p(out), ctypes.byref(st))
+        return out, int(st.value)
+
+
+class _Handle:
+    def __init__(self, checker, h, inst):
+        self.c, self.h, self.inst = checker, h, inst
+        self.E, self.R = inst.E, inst.R
+
+    def __del__(self):
+        try:
+            self.c._f("problem_destroy")(self.h)
+        except Exception:
+            pass
+
+    def derived(self):
+        E, R = self.E, self.R
+        sn = np.zeros(E, np.int32)
+        corr = np.zeros((E, E), np.int32)
+        poss = np.zeros((E, R), np.int32)
+        self.c._f("problem_derived")(self.h, _p(sn), _p(corr), _p(poss))
+        return sn, corr, poss
+
+    def eval(self, slot, room):
+        slot = np.ascontiguousarray(slot, np.uint8)
+        room = np.ascontiguousarray(room, np.uint8)
+        P = slot.shape[0]
+        hcv = np.zeros(P, np.int32); scv = np.zeros(P, np.int32)
+        feas = np.zeros(P, np.uint8); pen = np.zeros(P, np.int32)
+        self.c._f("eval")(self.h, _p(slot), _p(room), P, _p(hcv), _p(scv), _p(feas), _p(pen))
+        return hcv, scv, feas, pen
+
+    def assign_rooms(self, slot):
+        slot = np.ascontiguousarray(slot, np.uint8)
+        room = np.zeros_like(slot)
+        self.c._f("assign_rooms")(self.h, _p(slot), _p(room), slot.shape[0])
+        return room
+
+    def random_init(self, seeds):
+        rng = np.ascontiguousarray(seeds, np.int64).copy()
+        P = rng.size
+        slot = np.zeros((P, self.E), np.uint8); room = np.zeros((P, self.E), np.uint8)
+        self.c._f("random_init")(self.h, _p(rng), _p(slot), _p(room), P)
+        return slot, room, rng
+
+    def local_search(self, slot, room, seeds, max_steps, p1=1.0, p2=1.0, p3=0.0):
+        slot = np.ascontiguousarray(slot, np.uint8).copy()
+        room = np.ascontiguousarray(room, np.uint8).copy()
+        rng = np.ascontiguousarray(seeds, np.int64).copy()
+        self.c._f("local_search")(self.h, _p(slot), _p(room), _p(rng), slot.shape[0], int(max_steps),
+                                  float(p1), float(p2), float(p3))
+        return slot, room, rng
+
+    def crossover(self, s1, s2, seeds):
+        s1 = np.ascontiguousarray(s1, np.uint8); s2 = np.ascontiguousarray(s2, np.uint8)
+        rng = np.ascontiguousarray(seeds, np.int64).copy()
+        slot = np.zeros_like(s1); room = np.zeros_like(s1)
+        self.c._f("crossover")(self.h, _p(s1), _p(s2), _p(rng), _p(slot), _p(room), s1.shape[0])
+        return slot, room, rng
+
+    def mutation(self, slot, room, seeds):
+        slot = np.ascontiguousarray(slot, np.uint8).copy()
+        room = np.ascontiguousarray(room, np.uint8).copy()
+        rng = np.ascontiguousarray(seeds, np.int64).copy()
+        self.c._f("mutation")(self.h, _p(slot), _p(room), _p(rng), slot.shape[0])
+        return slot, room, rng
+
+
+class Oracle(_Checker):
+    prefix = "tto_"
+
+
+class Ref(_Checker):
+    prefix = "ref_"
+
+
+def oracle():
+    if not ORACLE_PATH.exists():
+        raise FileNotFoundError(f"{ORACLE_PATH} missing: run `make -C oracle oracle`")
+    return Oracle(ORACLE_PATH)
+
+
+def ref():
+    """The reference build, or None where it was never built (no /root/reference)."""
+    return Ref(REF_PATH) if REF_PATH.exists() else None

@@ -1,0 +1,180 @@
+"""GPU parity: every kernel through the C-ABI vs the reference's golden vectors
+and vs the CPU oracle on seeded inputs; size-independent properties at the
+benchmark size. Bit-exact (integer/byte/index work)."""
+import numpy as np
+import pytest
+
+import ttga
+from oracle_lib import oracle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+from ttga import native  # noqa: E402
+
+NAMES = ["sm", "med", "tight"]
+
+
+def load(golden_dir, name):
+    z = np.load(golden_dir / f"{name}.npz")
+    E, R, F, S = (int(x) for x in z["dims"])
+    inst = ttga.Instance(E, R, F, S, z["room_size"], z["student_events"], z["room_features"], z["event_features"])
+    return inst, z
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return oracle()
+
+
+@pytest.fixture(scope="module")
+def problems(golden_dir):
+    out = {}
+    for n in NAMES:
+        inst, z = load(golden_dir, n)
+        out[n] = (native.DeviceProblem(inst), inst, z)
+    return out
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_derived_matches_reference(problems, name):
+    dp, inst, z = problems[name]
+    sn, corr, poss = dp.derived()
+    assert np.array_equal(sn, z["ref_student_number"])
+    assert np.array_equal(np.packbits(corr.astype(np.uint8), axis=1), z["ref_corr_bits"])
+    assert np.array_equal(poss, z["ref_possible"])
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("tag,sk,rk", [("canon", "slots", "rooms"), ("rand", "slots", "rand_rooms"),
+                                       ("skew", "skew_slots", "skew_rooms"), ("edge", "edge_slots", "edge_rooms"),
+                                       ("ls3", "ls3_slots", "ls3_rooms")])
+def test_eval_golden(problems, name, tag, sk, rk, variant):
+    dp, inst, z = problems[name]
+    hcv, scv, feas, pen = (host(t) for t in dp.eval(dev(z[sk]), dev(z[rk]), variant=variant))
+    assert np.array_equal(hcv, z[f"eval_{tag}_hcv"])
+    assert np.array_equal(scv, z[f"eval_{tag}_scv"])
+    assert np.array_equal(feas, z[f"eval_{tag}_feasible"])
+    assert np.array_equal(pen, z[f"eval_{tag}_penalty"])
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_eval_random_vs_oracle(orc, variant):
+    inst = ttga.generate(333, 9, 6, 170, seed=11)      # E not a multiple of 4: byte staging path
+    dp = native.DeviceProblem(inst)
+    P = 203                                            # ragged last wave
+    slots, _ = ttga.random_slots(ttga.population_seeds(4242, P), inst.E)
+    rng = np.random.default_rng(5)
+    rooms = rng.integers(0, inst.R, size=(P, inst.E), dtype=np.uint8)
+    rooms[::3] = orc.problem(inst).assign_rooms(slots[::3])
+    got = [host(t) for t in dp.eval(dev(slots), dev(rooms), variant=variant)]
+    exp = orc.problem(inst).eval(slots, rooms)
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+
+
+def test_eval_invalid_individual_flagged(problems):
+    dp, inst, z = problems["sm"]
+    s = z["slots"][:3].copy()
+    r = z["rooms"][:3].copy()
+    s[1, 7] = 45
+    r[2, 3] = inst.R
+    for variant in (1, 2):
+        hcv, scv, feas, pen = (host(t) for t in dp.eval(dev(s), dev(r), variant=variant))
+        assert hcv[0] == z["eval_canon_hcv"][0]
+        assert list(hcv[1:]) == [-1, -1] and list(pen[1:]) == [-1, -1] and list(feas[1:]) == [0, 0]
+
+
+def test_eval_empty_population(problems):
+    dp, inst, z = problems["sm"]
+    e = torch.empty((0, inst.E), dtype=torch.uint8, device="cuda")
+    dp.eval(e, e)
+
+
+def test_eval_bench_size_properties(orc):
+    """P = 65536 on the headline instance: the two independent kernels agree on
+    every individual, a strided sample matches the oracle, and feasibility
+    <=> hcv == 0 with penalty = feasible ? scv : 1e6 + hcv."""
+    inst = ttga.config_instance("med")
+    dp = native.DeviceProblem(inst)
+    P = 65536
+    g = torch.Generator(device="cuda").manual_seed(0)
+    slot = torch.randint(0, 45, (P, inst.E), dtype=torch.uint8, device="cuda", generator=g)
+    room = dp.assign_rooms(slot)
+    a = [host(t) for t in dp.eval(slot, room, variant=1)]
+    b = [host(t) for t in dp.eval(slot, room, variant=2)]
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    hcv, scv, feas, pen = a
+    assert np.array_equal(feas.astype(bool), hcv == 0)
+    assert np.array_equal(pen, np.where(hcv == 0, scv, 1000000 + hcv))
+    idx = np.arange(0, P, 1021)
+    s_np, r_np = host(slot)[idx], host(room)[idx]
+    exp = orc.problem(inst).eval(s_np, r_np)
+    assert np.array_equal(orc.problem(inst).assign_rooms(s_np), r_np)
+    for x, e in zip(a, exp):
+        assert np.array_equal(x[idx], e)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_assign_rooms_golden(problems, name):
+    dp, inst, z = problems[name]
+    assert np.array_equal(host(dp.assign_rooms(dev(z["slots"]))), z["rooms"])
+    assert np.array_equal(host(dp.assign_rooms(dev(z["skew_slots"]))), z["skew_rooms"])   # N > 64 per slot
+    assert dp.status() == 0
+
+
+def test_assign_rooms_random_vs_oracle(orc):
+    for seed, dims in [(21, (250, 12, 4, 150)), (22, (600, 30, 6, 300))]:
+        inst = ttga.generate(*dims, seed=seed)
+        dp = native.DeviceProblem(inst)
+        slots, _ = ttga.random_slots(ttga.population_seeds(seed, 97), inst.E)
+        slots[:10] = (slots[:10] % 4) * 11     # crowded slots
+        assert np.array_equal(host(dp.assign_rooms(dev(slots))), orc.problem(inst).assign_rooms(slots))
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_random_init_crossover_mutation_golden(problems, name):
+    dp, inst, z = problems[name]
+    n = z["init_seeds"].size
+    rng = dev(z["init_seeds"]); s = dev(np.zeros((n, inst.E), np.uint8)); r = dev(np.zeros((n, inst.E), np.uint8))
+    dp.random_init(rng, s, r)
+    assert np.array_equal(host(s), z["init_slots"]) and np.array_equal(host(r), z["init_rooms"])
+    assert np.array_equal(host(rng), z["init_rng"])
+    h = n // 2
+    rng = dev(z["xover_seeds"]); cs = dev(np.zeros((h, inst.E), np.uint8)); cr = dev(np.zeros((h, inst.E), np.uint8))
+    dp.crossover(dev(z["init_slots"][:h]), dev(z["init_slots"][h:]), rng, cs, cr)
+    assert np.array_equal(host(cs), z["xover_slots"]) and np.array_equal(host(cr), z["xover_rooms"])
+    assert np.array_equal(host(rng), z["xover_rng"])
+    rng = dev(z["mut_seeds"]); ms = dev(z["init_slots"]); mr = dev(z["init_rooms"])
+    dp.mutation(ms, mr, rng)
+    assert np.array_equal(host(ms), z["mut_slots"]) and np.array_equal(host(mr), z["mut_rooms"])
+    assert np.array_equal(host(rng), z["mut_rng"])
+
+
+def test_syn_scale_instance(orc):
+    """Synthetic 2000/40/10/5000 instance (BASELINE configs[4]): the lane kernel
+    is out of range so tt_eval uses the workgroup kernel; spot-check vs oracle."""
+    inst = ttga.config_instance("syn")
+    dp = native.DeviceProblem(inst)
+    P = 512
+    slots, _ = ttga.random_slots(ttga.population_seeds(31, P), inst.E)
+    room = dp.assign_rooms(dev(slots))
+    hcv, scv, feas, pen = (host(t) for t in dp.eval(dev(slots), room))
+    idx = np.array([0, 1, 255, 511])
+    o = orc.problem(inst)
+    r_np = host(room)[idx]
+    assert np.array_equal(o.assign_rooms(slots[idx]), r_np)
+    exp = o.eval(slots[idx], r_np)
+    for x, e in zip((hcv, scv, feas, pen), exp):
+        assert np.array_equal(x[idx], e)

@@ -1,0 +1,147 @@
+"""The CPU restatement (oracle/) is pinned against the reference's own outputs.
+
+Golden vectors in tests/golden/ come from the reference's Problem/Solution
+objects (oracle/gen_golden.py). Where oracle/_ref/libttref.so exists, the
+restatement is additionally cross-checked on fresh random inputs.
+"""
+import numpy as np
+import pytest
+
+import ttga
+from oracle_lib import oracle, ref
+
+NAMES = ["sm", "med", "tight"]
+
+
+def load(golden_dir, name):
+    z = np.load(golden_dir / f"{name}.npz")
+    E, R, F, S = (int(x) for x in z["dims"])
+    inst = ttga.Instance(E, R, F, S, z["room_size"], z["student_events"], z["room_features"], z["event_features"])
+    return inst, z
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return oracle()
+
+
+def test_rng_known_answers(golden_dir, orc):
+    z = np.load(golden_dir / "rng.npz")
+    for seed, draws, final in zip(z["seeds"], z["draws"], z["finals"]):
+        d, f = orc.rand(int(seed), draws.size)
+        assert np.array_equal(d, draws) and f == final
+        r = ttga.ParkMiller(int(seed))
+        py = np.array([r.next() for _ in range(draws.size)])
+        assert np.array_equal(py, draws) and r.seed == final
+
+
+def test_random_slots_vectorised_matches_stream(golden_dir):
+    seeds = ttga.population_seeds(12345, 5)
+    slots, finals = ttga.random_slots(seeds, 50)
+    for i, s in enumerate(seeds):
+        r = ttga.ParkMiller(int(s))
+        assert [r.pick(45) for _ in range(50)] == slots[i].tolist()
+        assert r.seed == finals[i]
+
+
+def test_tim_roundtrip_and_derived(golden_dir, orc):
+    inst = ttga.read_tim(golden_dir / "sm.tim")
+    _, z = load(golden_dir, "sm")
+    assert np.array_equal(inst.student_events, z["student_events"])
+    assert inst.to_tim() == (golden_dir / "sm.tim").read_text()
+    sn, corr, poss = orc.problem(inst).derived()
+    assert np.array_equal(sn, z["ref_student_number"])
+    assert np.array_equal(np.packbits(corr.astype(np.uint8), axis=1), z["ref_corr_bits"])
+    assert np.array_equal(poss, z["ref_possible"])
+    # numpy restatement too
+    assert np.array_equal(inst.student_number(), sn)
+    assert np.array_equal(inst.correlations(), corr)
+    assert np.array_equal(inst.possible_rooms(), poss)
+
+
+def test_tim_parser_rejects_truncated():
+    with pytest.raises(ValueError):
+        ttga.parse_tim("3 1 0 2\n5\n1 0")
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_derived(golden_dir, orc, name):
+    inst, z = load(golden_dir, name)
+    sn, corr, poss = orc.problem(inst).derived()
+    assert np.array_equal(sn, z["ref_student_number"])
+    assert np.array_equal(np.packbits(corr.astype(np.uint8), axis=1), z["ref_corr_bits"])
+    assert np.array_equal(poss, z["ref_possible"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("tag,sk,rk", [("canon", "slots", "rooms"), ("rand", "slots", "rand_rooms"),
+                                       ("skew", "skew_slots", "skew_rooms"), ("edge", "edge_slots", "edge_rooms"),
+                                       ("ls3", "ls3_slots", "ls3_rooms")])
+def test_eval(golden_dir, orc, name, tag, sk, rk):
+    inst, z = load(golden_dir, name)
+    h = orc.problem(inst)
+    hcv, scv, feas, pen = h.eval(z[sk], z[rk])
+    assert np.array_equal(hcv, z[f"eval_{tag}_hcv"])
+    assert np.array_equal(scv, z[f"eval_{tag}_scv"])
+    assert np.array_equal(feas, z[f"eval_{tag}_feasible"])
+    assert np.array_equal(pen, z[f"eval_{tag}_penalty"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_assign_rooms(golden_dir, orc, name):
+    inst, z = load(golden_dir, name)
+    h = orc.problem(inst)
+    assert np.array_equal(h.assign_rooms(z["slots"]), z["rooms"])
+    assert np.array_equal(h.assign_rooms(z["skew_slots"]), z["skew_rooms"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_variation(golden_dir, orc, name):
+    inst, z = load(golden_dir, name)
+    h = orc.problem(inst)
+    s, r, g = h.random_init(z["init_seeds"])
+    assert np.array_equal(s, z["init_slots"]) and np.array_equal(r, z["init_rooms"])
+    assert np.array_equal(g, z["init_rng"])
+    n = z["init_slots"].shape[0] // 2
+    s, r, g = h.crossover(z["init_slots"][:n], z["init_slots"][n:], z["xover_seeds"])
+    assert np.array_equal(s, z["xover_slots"]) and np.array_equal(r, z["xover_rooms"])
+    assert np.array_equal(g, z["xover_rng"])
+    s, r, g = h.mutation(z["init_slots"], z["init_rooms"], z["mut_seeds"])
+    assert np.array_equal(s, z["mut_slots"]) and np.array_equal(r, z["mut_rooms"])
+    assert np.array_equal(g, z["mut_rng"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_local_search(golden_dir, orc, name):
+    inst, z = load(golden_dir, name)
+    h = orc.problem(inst)
+    n = z["ls_seeds"].size
+    s, r, g = h.local_search(z["init_slots"][:n], z["init_rooms"][:n], z["ls_seeds"], 200)
+    assert np.array_equal(s, z["ls_slots"]) and np.array_equal(r, z["ls_rooms"]) and np.array_equal(g, z["ls_rng"])
+    s, r, g = h.local_search(s, r, g, 1000)
+    assert np.array_equal(s, z["ls2_slots"]) and np.array_equal(r, z["ls2_rooms"]) and np.array_equal(g, z["ls2_rng"])
+    s, r, g = h.local_search(s, r, g, 2000)
+    assert np.array_equal(s, z["ls3_slots"]) and np.array_equal(r, z["ls3_rooms"]) and np.array_equal(g, z["ls3_rng"])
+    s, r, g = h.local_search(z["init_slots"][:4], z["init_rooms"][:4], ttga.population_seeds(9500, 4), 60, 1, 1, 1)
+    assert np.array_equal(s, z["lsp3_slots"]) and np.array_equal(r, z["lsp3_rooms"])
+    assert np.array_equal(g, z["lsp3_rng"])
+
+
+# ---- live cross-checks against the reference build (skipped where it was never built)
+REF = ref()
+needs_ref = pytest.mark.skipif(REF is None, reason="oracle/_ref not built (no /root/reference)")
+
+
+@needs_ref
+@pytest.mark.parametrize("seed", [3, 4])
+def test_oracle_vs_reference_random(orc, seed):
+    inst = ttga.generate(150, 6, 4, 120, seed=seed)
+    ho, hr = orc.problem(inst), REF.problem(inst)
+    slots, _ = ttga.random_slots(ttga.population_seeds(seed * 1000, 40), inst.E)
+    ro, rr = ho.assign_rooms(slots), hr.assign_rooms(slots)
+    assert np.array_equal(ro, rr)
+    for a, b in zip(ho.eval(slots, ro), hr.eval(slots, rr)):
+        assert np.array_equal(a, b)
+    seeds = ttga.population_seeds(seed * 77, 6)
+    for a, b in zip(ho.local_search(slots[:6], ro[:6], seeds, 300), hr.local_search(slots[:6], rr[:6], seeds, 300)):
+        assert np.array_equal(a, b)

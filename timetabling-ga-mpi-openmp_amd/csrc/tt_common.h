@@ -1,0 +1,54 @@
+// Shared device-side definitions for the ttga HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ttga {
+
+constexpr int kSlots = 45;             // Solution.cpp:52,57
+constexpr int kSlotsPerDay = 9;
+constexpr int kMaxRooms = 64;          // rooms are bitmasks in one 64-bit word
+constexpr int kMaxSlotEvents = 256;    // per-slot event bitsets (4 x 64 bits) in the matcher
+
+// slot s is the last of its day (s % 9 == 8): Solution.cpp:94
+constexpr uint64_t kLastSlotMask = (1ull << 8) | (1ull << 17) | (1ull << 26) | (1ull << 35) | (1ull << 44);
+// bit k set iff slots k, k+1, k+2 lie in one day (k % 9 <= 6): the >2-in-a-row window
+constexpr uint64_t kTripleMask = 0x7Full | (0x7Full << 9) | (0x7Full << 18) | (0x7Full << 27) | (0x7Full << 36);
+
+// Device image of a Problem (Problem.h:35-46), read-only for the handle's lifetime.
+struct DevProblem {
+    int E, R, S, EW;              // EW = 32-bit words per correlation row
+    const int32_t* sn;            // [E] studentNumber
+    const int32_t* stu_off;       // [S+1] CSR of student_events by student
+    const int32_t* stu_ev;        //   events of each student, ascending
+    const int32_t* ev_off;        // [E+1] CSR by event
+    const int32_t* ev_stu;        //   students of each event, ascending
+    const uint64_t* poss;         // [E] possibleRooms as room bitmasks
+    const uint32_t* corr;         // [E*EW] eventCorrelations bit-matrix (diagonal included)
+    const int32_t* cp_off;        // [E+1] upper-triangle correlation lists (j > i)
+    const int32_t* cp_j;
+    int32_t* status;              // device status word (tt_device_status)
+};
+
+// Park-Miller "minimal standard" generator, Schrage's method
+// (Random.h:15-19, Random.cc:27-37). Bit-exact with the reference: int64
+// state arithmetic, then AM * state in IEEE fp64 (gfx950 has full fp64).
+__device__ __forceinline__ double pm_next(int64_t& s) {
+    const int64_t IA = 16807, IM = 2147483647, IQ = 127773, IR = 2836;
+    const double AM = 1.0 / 2147483647.0;
+    int64_t k = s / IQ;
+    s = IA * (s - k * IQ) - IR * k;
+    if (s < 0) s += IM;
+    return __dmul_rn(AM, (double)s);
+}
+
+// (int)(next() * n): truncation of the fp64 product (Solution.cpp:52, ga.cpp:135)
+__device__ __forceinline__ int pm_pick(int64_t& s, int n) { return (int)__dmul_rn(pm_next(s), (double)n); }
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace ttga

@@ -1,0 +1,42 @@
+// Host-side internals shared by the C-ABI translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+#include "../../include/ttga.h"
+#include "tt_common.h"
+
+struct tt_problem {
+    int E, R, F, S, device;
+    // host copies (tt_problem_derived, validation)
+    std::vector<int32_t> student_number;
+    std::vector<uint64_t> poss_bits;
+    std::vector<uint32_t> corr_bits;
+    int nnz_students, nnz_pairs, max_cells;
+    // device allocations
+    void* dev_block;
+    ttga::DevProblem dev;
+};
+
+namespace ttga {
+
+void set_error(const std::string& msg);
+
+// Returns TT_OK or records the HIP error and returns TT_ERR_DEVICE.
+int check_hip(hipError_t e, const char* what);
+
+#define TT_HIP(call)                                         \
+    do {                                                     \
+        int _rc = ::ttga::check_hip((call), #call);          \
+        if (_rc != TT_OK) return _rc;                        \
+    } while (0)
+
+// Common argument checks for population entry points.
+int check_pop_args(const tt_problem* p, int P, const void* a, const void* b);
+
+// Makes the handle's device current for the calling thread.
+int use_device(const tt_problem* p);
+
+}  // namespace ttga

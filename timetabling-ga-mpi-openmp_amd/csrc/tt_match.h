@@ -1,0 +1,235 @@
+// Wave-level room assignment: Solution::assignRooms (Solution.cpp:772-891).
+//
+// The reference builds, per timeslot, a flow network source(1) -> events
+// (2..N+1) -> rooms (N+2..N+R+1) -> sink (V) with unit capacities and runs a
+// priority-first search (networkFlow) until no augmenting path remains. With
+// unit capacities every reachable node gets priority value -9 and unseen
+// nodes -10, so the search always expands the LOWEST-INDEX fringe node: all
+// fringe events (ascending), then fringe rooms (ascending), the sink last;
+// a node's dad is the first visited node with a residual edge to it, and the
+// augmenting path is fixed the moment the first FREE room is visited (its dad
+// chain never changes afterwards). This file replays exactly that search on
+// 64-bit bitsets (events of the slot, rooms), one LANE PER TIMESLOT, one WAVE
+// PER INDIVIDUAL. Read-out (Solution.cpp:802-830): matched events take their
+// room; unmatched events take the first possible room unless a possible room
+// is free (busy[] starts at 0), and an event with no possible room
+// keeps the carried-over lessBusy (initially 0, declared once per call).
+#pragma once
+#include "tt_common.h"
+
+namespace ttga {
+
+constexpr uint8_t kNone = 0xFF;
+
+// Per-wave LDS scratch for one individual.
+struct MatchScratch {
+    uint8_t* sl;        // [E]     slot of each event
+    uint8_t* rr;        // [E]     room of each event (output row)
+    uint16_t* bev;      // [E]     events bucketed by slot, ascending inside a slot
+    uint8_t* mr;        // [E]     matched room per bucket position (kNone)
+    uint64_t* pl;       // [E]     possible-room mask per bucket position
+    uint8_t* rm;        // [45*R]  event (bucket-local index) matched to each room
+    uint8_t* dr;        // [45*R]  dad (bucket-local event) of each room in the search
+    int32_t* bstart;    // [46]    bucket offsets
+    uint32_t* tmp;      // [64]
+    uint32_t* flags;    // [4]
+};
+
+__host__ __device__ inline size_t match_scratch_bytes(int E, int R) {
+    size_t b = 0;
+    b += (size_t)E;                          // sl
+    b += (size_t)E;                          // rr
+    b = (b + 1) & ~(size_t)1;
+    b += 2 * (size_t)E;                      // bev
+    b += (size_t)E;                          // mr
+    b = (b + 7) & ~(size_t)7;
+    b += 8 * (size_t)E;                      // pl
+    b += 2 * (size_t)kSlots * R;             // rm, dr
+    b = (b + 3) & ~(size_t)3;
+    b += 4 * 46 + 4 * 64 + 4 * 4;            // bstart, tmp, flags
+    return (b + 15) & ~(size_t)15;
+}
+
+__device__ inline MatchScratch carve_match_scratch(uint8_t* base, int E, int R) {
+    MatchScratch m;
+    size_t b = 0;
+    m.sl = base + b; b += E;
+    m.rr = base + b; b += E;
+    b = (b + 1) & ~(size_t)1;
+    m.bev = (uint16_t*)(base + b); b += 2 * (size_t)E;
+    m.mr = base + b; b += E;
+    b = (b + 7) & ~(size_t)7;
+    m.pl = (uint64_t*)(base + b); b += 8 * (size_t)E;
+    m.rm = base + b; b += (size_t)kSlots * R;
+    m.dr = base + b; b += (size_t)kSlots * R;
+    b = (b + 3) & ~(size_t)3;
+    m.bstart = (int32_t*)(base + b); b += 4 * 46;
+    m.tmp = (uint32_t*)(base + b); b += 4 * 64;
+    m.flags = (uint32_t*)(base + b);
+    return m;
+}
+
+__device__ __forceinline__ int wave_inclusive_scan(int v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
+
+// Bucket the events by slot, ascending event index inside each bucket
+// (the order of timeslot_events lists, which are always kept sorted).
+// All 64 lanes of the wave call this; sl[] must be filled.
+__device__ inline void build_buckets(const DevProblem& pb, MatchScratch& m, int lane) {
+    const int E = pb.E;
+    m.tmp[lane] = 0u;
+    __syncthreads();
+    for (int e = lane; e < E; e += 64) {
+        const int s = m.sl[e];
+        if (s < kSlots) atomicAdd(&m.tmp[s], 1u);
+    }
+    __syncthreads();
+    const int c = lane < kSlots ? (int)m.tmp[lane] : 0;
+    const int incl = wave_inclusive_scan(c, lane);
+    const int start = incl - c;
+    if (lane < kSlots) m.bstart[lane] = start;
+    if (lane == kSlots - 1) m.bstart[kSlots] = incl;
+    // stable fill: lane t walks the slot row (broadcast reads) and keeps its events
+    int pos = start;
+    int e = 0;
+    const int me = lane < kSlots ? lane : 0x100;     // lanes >= 45 never match a byte
+    for (; e + 4 <= E; e += 4) {
+        uint32_t w = (uint32_t)m.sl[e] | ((uint32_t)m.sl[e + 1] << 8) | ((uint32_t)m.sl[e + 2] << 16) |
+                     ((uint32_t)m.sl[e + 3] << 24);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if ((int)((w >> (8 * k)) & 0xFFu) == me) m.bev[pos++] = (uint16_t)(e + k);
+    }
+    for (; e < E; ++e)
+        if (m.sl[e] == me) m.bev[pos++] = (uint16_t)e;
+    __syncthreads();
+    const int nb = m.bstart[kSlots];
+    for (int b = lane; b < nb; b += 64) m.pl[b] = pb.poss[m.bev[b]];
+    __syncthreads();
+}
+
+template <int NW>
+__device__ __forceinline__ int pop_lowest(uint64_t (&f)[NW]) {
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        if (f[w]) {
+            const int b = __builtin_ctzll(f[w]);
+            f[w] &= f[w] - 1;
+            return 64 * w + b;
+        }
+    }
+    return -1;
+}
+
+// Max-cardinality matching + read-out for one slot (N events, N <= 64*NW).
+template <int NW>
+__device__ void match_slot(int R, const uint16_t* ev, const uint64_t* pl, int N, uint8_t* mr, uint8_t* rm,
+                           uint8_t* dr, uint8_t* rr) {
+    uint64_t unm[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        const int lo = 64 * w;
+        unm[w] = N >= lo + 64 ? ~0ull : (N > lo ? ((1ull << (N - lo)) - 1ull) : 0ull);
+    }
+    for (int i = 0; i < N; ++i) mr[i] = kNone;
+    uint64_t rmatched = 0;
+    for (;;) {
+        // networkFlow (Solution.cpp:852-891): lowest-index-first search from the source
+        uint64_t se[NW], fe[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) { se[w] = unm[w]; fe[w] = unm[w]; }
+        uint64_t sr = 0, fr = 0;
+        int sink = -1;
+        for (;;) {
+            const int i = pop_lowest<NW>(fe);
+            if (i >= 0) {                              // expand event i: forward residual edges
+                const uint64_t own = mr[i] != kNone ? (1ull << mr[i]) : 0ull;
+                uint64_t nr = pl[i] & ~sr & ~own;
+                sr |= nr;
+                fr |= nr;
+                while (nr) {
+                    const int j = __builtin_ctzll(nr);
+                    nr &= nr - 1;
+                    dr[j] = (uint8_t)i;
+                }
+                continue;
+            }
+            if (fr) {                                  // expand room j
+                const int j = __builtin_ctzll(fr);
+                fr &= fr - 1;
+                if (!((rmatched >> j) & 1ull)) { sink = j; break; }   // free room: path to the sink is fixed
+                const int i2 = rm[j];                  // reverse edge to its matched event
+                const uint64_t b = 1ull << (i2 & 63);
+#pragma unroll
+                for (int w = 0; w < NW; ++w)
+                    if (w == (i2 >> 6) && !(se[w] & b)) { se[w] |= b; fe[w] |= b; }
+                continue;
+            }
+            break;
+        }
+        if (sink < 0) break;
+        // maxMatching augmentation (Solution.cpp:836-849)
+        int j = sink;
+        for (;;) {
+            const int i = dr[j];
+            const int prev = mr[i];
+            mr[i] = (uint8_t)j;
+            rm[j] = (uint8_t)i;
+            rmatched |= 1ull << j;
+            if (prev == kNone) {
+#pragma unroll
+                for (int w = 0; w < NW; ++w)
+                    if (w == (i >> 6)) unm[w] &= ~(1ull << (i & 63));
+                break;
+            }
+            j = prev;
+        }
+    }
+    // read-out and unplaced events (Solution.cpp:802-830)
+    int less_busy = 0;
+    for (int i = 0; i < N; ++i) {
+        int r = mr[i];
+        if (r == kNone) {
+            const uint64_t ps = pl[i];
+            if (ps) {
+                less_busy = __builtin_ctzll(ps);
+                if ((rmatched >> less_busy) & 1ull) {
+                    const uint64_t fr2 = ps & ~rmatched;
+                    if (fr2) less_busy = __builtin_ctzll(fr2);
+                }
+            }
+            r = less_busy;
+        }
+        rr[ev[i]] = (uint8_t)r;
+    }
+}
+
+// Re-assign rooms for every slot t with bit t of `touched` set and a
+// non-empty bucket. m.sl and m.rr hold the individual's row; rooms of
+// untouched slots in m.rr are left as they are. Buckets must be built.
+__device__ inline void assign_touched(const DevProblem& pb, MatchScratch& m, uint64_t touched, int lane) {
+    if (lane < kSlots && ((touched >> lane) & 1ull)) {
+        const int b0 = m.bstart[lane];
+        const int N = m.bstart[lane + 1] - b0;
+        const int R = pb.R;
+        if (N > 0) {
+            if (N <= 64)
+                match_slot<1>(R, m.bev + b0, m.pl + b0, N, m.mr + b0, m.rm + lane * R, m.dr + lane * R, m.rr);
+            else if (N <= kMaxSlotEvents)
+                match_slot<4>(R, m.bev + b0, m.pl + b0, N, m.mr + b0, m.rm + lane * R, m.dr + lane * R, m.rr);
+            else {
+                for (int i = 0; i < N; ++i) m.rr[m.bev[b0 + i]] = 0xFF;
+                atomicOr(pb.status, 1);
+            }
+        }
+    }
+    __syncthreads();
+}
+
+}  // namespace ttga

@@ -1,0 +1,200 @@
+// Problem image: parse-free construction from .tim matrices, derived data
+// (Problem.cpp:86-148) and the device upload that replaces the reference's
+// MPI_Pack/MPI_Bcast of the Problem (ga.cpp:264-309,417-426).
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "tt_internal.h"
+
+namespace ttga {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int check_hip(hipError_t e, const char* what) {
+    if (e == hipSuccess) return TT_OK;
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return TT_ERR_DEVICE;
+}
+
+int check_pop_args(const tt_problem* p, int P, const void* a, const void* b) {
+    if (!p) { set_error("null tt_problem"); return TT_ERR_INVALID; }
+    if (P < 0) { set_error("negative population size"); return TT_ERR_INVALID; }
+    if (P > 0 && (!a || !b)) { set_error("null population buffer"); return TT_ERR_INVALID; }
+    return TT_OK;
+}
+
+int use_device(const tt_problem* p) {
+    int cur = -1;
+    TT_HIP(hipGetDevice(&cur));
+    if (cur != p->device) TT_HIP(hipSetDevice(p->device));
+    return TT_OK;
+}
+
+}  // namespace ttga
+
+using namespace ttga;
+
+extern "C" {
+
+int tt_version(void) { return 1; }
+
+const char* tt_last_error(void) { return g_last_error.c_str(); }
+
+int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, const int32_t* A,
+                      const int32_t* room_feat, const int32_t* event_feat, int device, tt_problem** out) {
+    if (!out) { set_error("null output handle"); return TT_ERR_INVALID; }
+    *out = nullptr;
+    if (E < 1 || E > 65535 || R < 1 || F < 0 || S < 0) { set_error("bad instance dimensions"); return TT_ERR_INVALID; }
+    if (R > kMaxRooms) { set_error("more than 64 rooms is not supported"); return TT_ERR_LIMIT; }
+    if (!room_size || (S > 0 && !A) || (F > 0 && (!room_feat || !event_feat))) {
+        set_error("null instance matrix");
+        return TT_ERR_INVALID;
+    }
+    for (long i = 0; i < (long)S * E; i++)
+        if (A[i] != 0 && A[i] != 1) { set_error("student_events must be 0/1"); return TT_ERR_INVALID; }
+    for (long i = 0; i < (long)R * F; i++)
+        if (room_feat[i] != 0 && room_feat[i] != 1) { set_error("room_features must be 0/1"); return TT_ERR_INVALID; }
+    for (long i = 0; i < (long)E * F; i++)
+        if (event_feat[i] != 0 && event_feat[i] != 1) { set_error("event_features must be 0/1"); return TT_ERR_INVALID; }
+
+    tt_problem* p = new tt_problem();
+    p->E = E; p->R = R; p->F = F; p->S = S; p->device = device;
+    const int EW = (E + 31) / 32;
+
+    // studentNumber (Problem.cpp:87-93) and the two CSR views of student_events.
+    std::vector<int32_t> stu_off(S + 1, 0), stu_ev, ev_off(E + 1, 0), ev_stu;
+    p->student_number.assign(E, 0);
+    for (int s = 0; s < S; s++) {
+        for (int e = 0; e < E; e++)
+            if (A[(long)s * E + e]) { stu_ev.push_back(e); p->student_number[e]++; }
+        stu_off[s + 1] = (int32_t)stu_ev.size();
+    }
+    for (int e = 0; e < E; e++) ev_off[e + 1] = ev_off[e] + p->student_number[e];
+    ev_stu.resize(stu_ev.size());
+    {
+        std::vector<int32_t> cur(ev_off.begin(), ev_off.end() - 1);
+        for (int s = 0; s < S; s++)
+            for (int k = stu_off[s]; k < stu_off[s + 1]; k++) ev_stu[cur[stu_ev[k]]++] = s;
+    }
+    // eventCorrelations (Problem.cpp:96-111): i ~ j iff a student attends both
+    // (diagonal set for events with students). Built student-major.
+    p->corr_bits.assign((size_t)E * EW, 0u);
+    for (int s = 0; s < S; s++)
+        for (int a = stu_off[s]; a < stu_off[s + 1]; a++)
+            for (int b = stu_off[s]; b < stu_off[s + 1]; b++) {
+                int i = stu_ev[a], j = stu_ev[b];
+                p->corr_bits[(size_t)i * EW + (j >> 5)] |= 1u << (j & 31);
+            }
+    std::vector<int32_t> cp_off(E + 1, 0), cp_j;
+    for (int i = 0; i < E; i++) {
+        for (int j = i + 1; j < E; j++)
+            if (p->corr_bits[(size_t)i * EW + (j >> 5)] >> (j & 31) & 1u) cp_j.push_back(j);
+        cp_off[i + 1] = (int32_t)cp_j.size();
+    }
+    // possibleRooms (Problem.cpp:130-148): size fits and every required feature present.
+    p->poss_bits.assign(E, 0ull);
+    for (int i = 0; i < E; i++)
+        for (int j = 0; j < R; j++) {
+            if (room_size[j] < p->student_number[i]) continue;
+            bool ok = true;
+            for (int k = 0; k < F && ok; k++)
+                if (event_feat[(long)i * F + k] == 1 && room_feat[(long)j * F + k] == 0) ok = false;
+            if (ok) p->poss_bits[i] |= 1ull << j;
+        }
+    p->nnz_students = (int)stu_ev.size();
+    p->nnz_pairs = (int)cp_j.size();
+
+    // One device block, 256-B aligned sub-buffers.
+    struct Part { const void* src; size_t bytes; size_t off; };
+    std::vector<Part> parts = {
+        {p->student_number.data(), sizeof(int32_t) * E, 0},
+        {stu_off.data(), sizeof(int32_t) * (S + 1), 0},
+        {stu_ev.data(), sizeof(int32_t) * stu_ev.size(), 0},
+        {ev_off.data(), sizeof(int32_t) * (E + 1), 0},
+        {ev_stu.data(), sizeof(int32_t) * ev_stu.size(), 0},
+        {p->poss_bits.data(), sizeof(uint64_t) * E, 0},
+        {p->corr_bits.data(), sizeof(uint32_t) * p->corr_bits.size(), 0},
+        {cp_off.data(), sizeof(int32_t) * (E + 1), 0},
+        {cp_j.data(), sizeof(int32_t) * cp_j.size(), 0},
+        {nullptr, sizeof(int32_t) * 4, 0},   // status word
+    };
+    size_t total = 0;
+    for (auto& q : parts) { q.off = total; total += (q.bytes + 255) & ~(size_t)255; }
+    total = std::max<size_t>(total, 256);
+
+    int prev = 0;
+    hipError_t he = hipGetDevice(&prev);
+    if (he == hipSuccess) he = hipSetDevice(device);
+    if (he == hipSuccess) he = hipMalloc(&p->dev_block, total);
+    if (he != hipSuccess) { check_hip(he, "tt_problem_create"); delete p; return TT_ERR_DEVICE; }
+    std::vector<uint8_t> staging(total, 0);
+    for (auto& q : parts)
+        if (q.src && q.bytes) memcpy(staging.data() + q.off, q.src, q.bytes);
+    he = hipMemcpy(p->dev_block, staging.data(), total, hipMemcpyHostToDevice);
+    if (he != hipSuccess) { check_hip(he, "tt_problem_create upload"); (void)hipFree(p->dev_block); delete p; return TT_ERR_DEVICE; }
+    (void)hipSetDevice(prev);
+
+    uint8_t* base = (uint8_t*)p->dev_block;
+    DevProblem& d = p->dev;
+    d.E = E; d.R = R; d.S = S; d.EW = EW;
+    d.sn = (const int32_t*)(base + parts[0].off);
+    d.stu_off = (const int32_t*)(base + parts[1].off);
+    d.stu_ev = (const int32_t*)(base + parts[2].off);
+    d.ev_off = (const int32_t*)(base + parts[3].off);
+    d.ev_stu = (const int32_t*)(base + parts[4].off);
+    d.poss = (const uint64_t*)(base + parts[5].off);
+    d.corr = (const uint32_t*)(base + parts[6].off);
+    d.cp_off = (const int32_t*)(base + parts[7].off);
+    d.cp_j = (const int32_t*)(base + parts[8].off);
+    d.status = (int32_t*)(base + parts[9].off);
+    *out = p;
+    return TT_OK;
+}
+
+int tt_problem_destroy(tt_problem* p) {
+    if (!p) return TT_OK;
+    int rc = TT_OK;
+    if (p->dev_block) {
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(p->device);
+        rc = check_hip(hipFree(p->dev_block), "tt_problem_destroy");
+        (void)hipSetDevice(prev);
+    }
+    delete p;
+    return rc;
+}
+
+int tt_problem_dims(const tt_problem* p, int32_t* dims) {
+    if (!p || !dims) { set_error("null argument"); return TT_ERR_INVALID; }
+    dims[0] = p->E; dims[1] = p->R; dims[2] = p->F; dims[3] = p->S;
+    return TT_OK;
+}
+
+int tt_problem_derived(const tt_problem* p, int32_t* student_number, int32_t* corr, int32_t* possible) {
+    if (!p) { set_error("null tt_problem"); return TT_ERR_INVALID; }
+    const int E = p->E, R = p->R, EW = (E + 31) / 32;
+    if (student_number) std::copy(p->student_number.begin(), p->student_number.end(), student_number);
+    if (corr)
+        for (int i = 0; i < E; i++)
+            for (int j = 0; j < E; j++) corr[(size_t)i * E + j] = (p->corr_bits[(size_t)i * EW + (j >> 5)] >> (j & 31)) & 1u;
+    if (possible)
+        for (int i = 0; i < E; i++)
+            for (int j = 0; j < R; j++) possible[(size_t)i * R + j] = (int32_t)((p->poss_bits[i] >> j) & 1ull);
+    return TT_OK;
+}
+
+int tt_device_status(const tt_problem* p, int32_t* status) {
+    if (!p || !status) { set_error("null argument"); return TT_ERR_INVALID; }
+    int rc = use_device(p);
+    if (rc) return rc;
+    TT_HIP(hipDeviceSynchronize());
+    TT_HIP(hipMemcpy(status, p->dev.status, sizeof(int32_t), hipMemcpyDeviceToHost));
+    return TT_OK;
+}
+
+}  // extern "C"

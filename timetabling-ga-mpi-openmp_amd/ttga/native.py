@@ -1,0 +1,184 @@
+"""ctypes binding of libttga.so (include/ttga.h) for device-resident populations.
+
+There is no CPU fallback anywhere in this module: if the HIP library is missing
+or the device calls fail, every entry point raises. Tensors are torch CUDA
+(=HIP) tensors; calls are enqueued on torch's current stream of the tensor's
+device.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import pathlib
+
+import numpy as np
+
+PKG_DIR = pathlib.Path(__file__).resolve().parent.parent
+LIB_PATH = PKG_DIR / "libttga.so"
+
+TT_OK, TT_ERR_INVALID, TT_ERR_DEVICE, TT_ERR_LIMIT = 0, 1, 2, 3
+NUM_SLOTS = 45
+
+EXPORTS = (
+    "tt_problem_create", "tt_problem_destroy", "tt_problem_dims", "tt_problem_derived", "tt_eval",
+    "tt_eval_variant", "tt_assign_rooms", "tt_random_init", "tt_crossover", "tt_mutation", "tt_local_search",
+    "tt_device_status", "tt_last_error", "tt_version",
+)
+
+_lib = None
+
+
+class TTError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"ttga error {code}: {msg}")
+        self.code = code
+
+
+def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
+    """Load libttga.so (built in-tree by `make -C timetabling-ga-mpi-openmp_amd`)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = pathlib.Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise FileNotFoundError(f"{p} not built: run `make -C {PKG_DIR}` (hipcc --offload-arch=gfx950)")
+    lib = ctypes.CDLL(str(p))
+    vp, i32, dbl = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+    P = ctypes.POINTER
+    lib.tt_problem_create.argtypes = [i32, i32, i32, i32, vp, vp, vp, vp, i32, P(vp)]
+    lib.tt_problem_destroy.argtypes = [vp]
+    lib.tt_problem_dims.argtypes = [vp, vp]
+    lib.tt_problem_derived.argtypes = [vp, vp, vp, vp]
+    lib.tt_eval.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, vp]
+    lib.tt_eval_variant.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, i32, vp]
+    lib.tt_assign_rooms.argtypes = [vp, vp, vp, i32, vp]
+    lib.tt_random_init.argtypes = [vp, vp, vp, vp, i32, vp]
+    lib.tt_crossover.argtypes = [vp, vp, vp, vp, vp, vp, i32, vp]
+    lib.tt_mutation.argtypes = [vp, vp, vp, vp, i32, vp]
+    lib.tt_local_search.argtypes = [vp, vp, vp, vp, i32, i32, dbl, dbl, dbl, vp]
+    lib.tt_device_status.argtypes = [vp, vp]
+    lib.tt_last_error.restype = ctypes.c_char_p
+    lib.tt_last_error.argtypes = []
+    lib.tt_version.argtypes = []
+    for name in EXPORTS:
+        if name not in ("tt_last_error",):
+            getattr(lib, name).restype = ctypes.c_int
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(lib, rc: int):
+    if rc != TT_OK:
+        raise TTError(rc, lib.tt_last_error().decode(errors="replace"))
+
+
+def _np_ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class DeviceProblem:
+    """A tt_problem handle: the Problem image resident on one GPU."""
+
+    def __init__(self, inst, device: int = 0):
+        self.lib = load()
+        self.inst = inst
+        self.device = device
+        self.E, self.R, self.F, self.S = inst.E, inst.R, inst.F, inst.S
+        h = ctypes.c_void_p()
+        rs, A = inst.room_size, inst.student_events
+        rf, ef = inst.room_features, inst.event_features
+        _check(self.lib, self.lib.tt_problem_create(self.E, self.R, self.F, self.S, _np_ptr(rs), _np_ptr(A),
+                                                    _np_ptr(rf), _np_ptr(ef), device, ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.tt_problem_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def derived(self):
+        sn = np.zeros(self.E, np.int32)
+        corr = np.zeros((self.E, self.E), np.int32)
+        poss = np.zeros((self.E, self.R), np.int32)
+        _check(self.lib, self.lib.tt_problem_derived(self.handle, _np_ptr(sn), _np_ptr(corr), _np_ptr(poss)))
+        return sn, corr, poss
+
+    def status(self) -> int:
+        v = ctypes.c_int32(0)
+        _check(self.lib, self.lib.tt_device_status(self.handle, ctypes.byref(v)))
+        return int(v.value)
+
+    # -- population operations (torch tensors on this device) -------------------
+    @staticmethod
+    def _stream(t):
+        import torch
+        return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+    def _pop(self, slot, room=None):
+        import torch
+        for t in (slot, room):
+            if t is None:
+                continue
+            if not (t.is_cuda and t.dtype == torch.uint8 and t.is_contiguous() and t.dim() == 2 and t.shape[1] == self.E):
+                raise ValueError("population tensors must be contiguous uint8 CUDA tensors of shape [P, E]")
+        return slot.shape[0]
+
+    def eval(self, slot, room, variant: int = 0, out=None):
+        import torch
+        P = self._pop(slot, room)
+        if out is None:
+            dev = slot.device
+            out = (torch.empty(P, dtype=torch.int32, device=dev), torch.empty(P, dtype=torch.int32, device=dev),
+                   torch.empty(P, dtype=torch.uint8, device=dev), torch.empty(P, dtype=torch.int32, device=dev))
+        hcv, scv, feas, pen = out
+        _check(self.lib, self.lib.tt_eval_variant(self.handle, slot.data_ptr(), room.data_ptr(), P, hcv.data_ptr(),
+                                                  scv.data_ptr(), feas.data_ptr(), pen.data_ptr(), variant,
+                                                  self._stream(slot)))
+        return out
+
+    def assign_rooms(self, slot, room=None):
+        import torch
+        P = self._pop(slot, room)
+        if room is None:
+            room = torch.empty_like(slot)
+        _check(self.lib, self.lib.tt_assign_rooms(self.handle, slot.data_ptr(), room.data_ptr(), P, self._stream(slot)))
+        return room
+
+    def random_init(self, rng, slot, room):
+        P = self._pop(slot, room)
+        self._rng(rng, P)
+        _check(self.lib, self.lib.tt_random_init(self.handle, rng.data_ptr(), slot.data_ptr(), room.data_ptr(), P,
+                                                 self._stream(slot)))
+
+    def crossover(self, slot1, slot2, rng, slot, room):
+        P = self._pop(slot, room)
+        self._pop(slot1, slot2)
+        self._rng(rng, P)
+        _check(self.lib, self.lib.tt_crossover(self.handle, slot1.data_ptr(), slot2.data_ptr(), rng.data_ptr(),
+                                               slot.data_ptr(), room.data_ptr(), P, self._stream(slot)))
+
+    def mutation(self, slot, room, rng):
+        P = self._pop(slot, room)
+        self._rng(rng, P)
+        _check(self.lib, self.lib.tt_mutation(self.handle, slot.data_ptr(), room.data_ptr(), rng.data_ptr(), P,
+                                              self._stream(slot)))
+
+    def local_search(self, slot, room, rng, max_steps: int, p1=1.0, p2=1.0, p3=0.0):
+        P = self._pop(slot, room)
+        self._rng(rng, P)
+        _check(self.lib, self.lib.tt_local_search(self.handle, slot.data_ptr(), room.data_ptr(), rng.data_ptr(), P,
+                                                  int(max_steps), float(p1), float(p2), float(p3),
+                                                  self._stream(slot)))
+
+    @staticmethod
+    def _rng(rng, P):
+        import torch
+        if not (rng.is_cuda and rng.dtype == torch.int64 and rng.is_contiguous() and rng.numel() == P):
+            raise ValueError("rng must be a contiguous int64 CUDA tensor with one state per individual")
