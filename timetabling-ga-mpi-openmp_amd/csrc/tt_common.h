@@ -27,6 +27,11 @@ struct DevProblem {
     const uint32_t* corr;         // [E*EW] eventCorrelations bit-matrix (diagonal included)
     const int32_t* cp_off;        // [E+1] upper-triangle correlation lists (j > i)
     const int32_t* cp_j;
+    int EW64;                     // 64-bit words per event bitset
+    const uint64_t* cupT;         // [EW64][E] upper-triangle correlation bits, word-major:
+                                  //   cupT[w*E+i] bit b <=> corr(i, 64w+b) and 64w+b > i
+    const int32_t* stc_off;       // [S+1] per-student event lists padded to multiples of 8
+    const int32_t* stc_ev;        //   padding entries hold E (a sentinel column)
     int32_t* status;              // device status word (tt_device_status)
 };
 

@@ -14,119 +14,169 @@
 //   feasible <=> hcv == 0 (Solution.cpp:63-84 tests the same three conditions).
 //
 // Two kernels:
-//  * eval_lanes (E <= 1024): one wave per 64 individuals. The individuals'
-//    slot rows are staged in LDS with an odd-dword row stride; the per-student
-//    attendance masks, the last-slot term and the correlated-pair term run
-//    LANE = INDIVIDUAL with wave-uniform loops over the problem's sparse
-//    structure (scalar loads, no divergence, conflict-free ds_read_u8); the
-//    room-clash term runs WAVE = INDIVIDUAL with LDS atomic cell counters.
+//  * eval_tile (E <= 1024): one workgroup per tile of 64 individuals, mixing a
+//    lane-per-individual phase (attendance masks) with a wave-per-individual
+//    phase (bitset hcv terms); see below.
 //  * eval_block (any E): one 256-thread workgroup per individual; slot
 //    buckets in LDS enumerate only same-slot pairs for the correlation term.
+#include <algorithm>
+
 #include "tt_internal.h"
 
 namespace ttga {
 
-// ---------------------------------------------------------------- eval_lanes
-__global__ __launch_bounds__(64) void eval_lanes_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
-                                                        const uint8_t* __restrict__ room, int P, int SP,
-                                                        int32_t* __restrict__ hcv_out, int32_t* __restrict__ scv_out,
-                                                        uint8_t* __restrict__ feas_out, int32_t* __restrict__ pen_out) {
+// ---------------------------------------------------------------- eval_tile
+// One workgroup of kTileWaves waves per tile of 64 individuals (persistent
+// over tiles). The tile's slot rows sit in LDS with an odd-dword row stride
+// plus a sentinel column E (slot 63, outside every day mask).
+//  * lane phase (LANE = INDIVIDUAL): wave w builds the 45-bit attendance mask
+//    of students w, w+8, ... from 8-padded event lists (8 independent
+//    conflict-free ds_read_u8 per chunk) -> >2-in-a-row and single-class terms;
+//  * wave phase (WAVE = INDIVIDUAL): per-slot event bitsets B[t] (ds_or_b64),
+//    room-cell counters (ds_add_rtn), unsuitable rooms, last-slot term, and the
+//    correlated same-slot pairs as popcount(cupT[w][i] & B[slot_i][w]) over the
+//    upper-triangle words (1.6 K word ops per individual at E=400 instead of
+//    13 K neighbour lookups).
+constexpr int kTileWaves = 8;
+
+struct TileLayout {
+    int SP;           // tile row stride (bytes)
+    int WS;           // per-wave scratch bytes
+    size_t off_wave;  // start of per-wave scratch
+    size_t off_part;  // [kTileWaves][64] lane-phase partials, then hq[64], sq[64]
+    size_t bytes;
+};
+
+__host__ __device__ inline TileLayout tile_layout(int E, int R) {
+    TileLayout L;
+    int sp = (E + 1 + 3) & ~3;                 // room for the sentinel column
+    if (((sp >> 2) & 1) == 0) sp += 4;         // odd dword stride: conflict-free column reads
+    L.SP = sp;
+    const int ew64 = (E + 63) / 64;
+    L.WS = (kSlots * ew64 * 8 + kSlots * R * 4 + 15) & ~15;
+    L.off_wave = ((size_t)64 * sp + 15) & ~(size_t)15;
+    L.off_part = L.off_wave + (size_t)kTileWaves * L.WS;
+    L.bytes = L.off_part + 4 * (size_t)(kTileWaves * 64 + 128);
+    return L;
+}
+
+__global__ __launch_bounds__(64 * kTileWaves) void eval_tile_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
+                                                                     const uint8_t* __restrict__ room, int P,
+                                                                     int32_t* __restrict__ hcv_out,
+                                                                     int32_t* __restrict__ scv_out,
+                                                                     uint8_t* __restrict__ feas_out,
+                                                                     int32_t* __restrict__ pen_out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int E = pb.E, R = pb.R, S = pb.S;
-    const int lane = threadIdx.x;
-    const long p0 = (long)blockIdx.x * 64;
-    const int np = (int)min((long)64, (long)P - p0);
-    uint8_t* tile = lds;                                           // [64][SP] slot rows
-    uint32_t* cnt = (uint32_t*)(lds + 64 * SP);                    // [45*R] cell counters
-    int32_t* xfer = (int32_t*)(cnt + ((kSlots * R + 3) & ~3));     // [64] room-term per individual
+    const int E = pb.E, R = pb.R, S = pb.S, EW64 = pb.EW64;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const TileLayout L = tile_layout(E, R);
+    const int SP = L.SP;
+    uint8_t* tile = lds;
+    uint64_t* B = (uint64_t*)(lds + L.off_wave + (size_t)wv * L.WS);   // [45][EW64]
+    uint32_t* cnt = (uint32_t*)(B + kSlots * EW64);                     // [45*R]
+    int32_t* part = (int32_t*)(lds + L.off_part);                       // [kTileWaves][64]
+    int32_t* hq = part + kTileWaves * 64;                               // [64]
+    int32_t* sq = hq + 64;                                              // [64]
+    const int tiles = (P + 63) / 64;
+    const int nthr = 64 * kTileWaves;
 
-    // ---- stage the slot rows of this wave's individuals into LDS
-    const uint8_t* src = slot + p0 * E;
-    if ((E & 3) == 0) {
-        const int wpr = E >> 2;
-        const uint32_t* s32 = (const uint32_t*)src;
-        const int nw = np * wpr;
-        for (int w = lane; w < nw; w += 64) {
-            int r = w / wpr, c = w - r * wpr;
-            *(uint32_t*)(tile + r * SP + 4 * c) = s32[w];
-        }
-    } else {
-        const int nb = np * E;
-        for (int b = lane; b < nb; b += 64) {
-            int r = b / E, c = b - r * E;
-            tile[r * SP + c] = src[b];
-        }
-    }
-    __syncthreads();
-
-    // ---- lane = individual (lanes >= np read a stale row; their results are dropped)
-    const uint8_t* my = tile + lane * SP;
-    int last = 0, cons = 0, single = 0, corr = 0;
-
-    // last slot of the day: Solution.cpp:93-96
-#pragma unroll 4
-    for (int e = 0; e < E; ++e) {
-        int s = my[e];
-        last += ((kLastSlotMask >> s) & 1ull) ? pb.sn[e] : 0;
-    }
-
-    // per-student attendance masks: Solution.cpp:98-137
-    for (int st = 0; st < S; ++st) {
-        const int k0 = pb.stu_off[st], k1 = pb.stu_off[st + 1];
-        uint64_t m = 0;
-        for (int k = k0; k < k1; ++k) m |= 1ull << my[pb.stu_ev[k]];
-        cons += __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);
-#pragma unroll
-        for (int d = 0; d < 5; ++d) {
-            uint32_t f = (uint32_t)(m >> (9 * d)) & 0x1FFu;
-            single += (__popc(f) == 1);
-        }
-    }
-
-    // correlated events in one slot: Solution.cpp:151-153
-    for (int i = 0; i < E; ++i) {
-        const int k0 = pb.cp_off[i], k1 = pb.cp_off[i + 1];
-        if (k0 == k1) continue;
-        const int si = my[i];
-        int c = 0;
-#pragma unroll 4
-        for (int k = k0; k < k1; ++k) c += (my[pb.cp_j[k]] == si);
-        corr += c;
-    }
-
-    // ---- wave = individual: room clashes (Solution.cpp:148-150) and unsuitable rooms (:155-156)
-    const int cells = kSlots * R;
-    for (int q = 0; q < np; ++q) {
-        for (int c = lane; c < cells; c += 64) cnt[c] = 0u;
+    for (int tl = blockIdx.x; tl < tiles; tl += gridDim.x) {
+        const long p0 = (long)tl * 64;
+        const int np = (int)min((long)64, (long)P - p0);
         __syncthreads();
-        const uint8_t* rs = tile + q * SP;
-        const uint8_t* rr = room + (p0 + q) * E;
-        int acc = 0;
-        bool bad = false;
-        for (int e = lane; e < E; e += 64) {
-            const int s = rs[e], r = rr[e];
-            if (s >= kSlots || r >= R) { bad = true; continue; }
-            acc += (int)atomicAdd(&cnt[s * R + r], 1u);
-            acc += ((pb.poss[e] >> r) & 1ull) ? 0 : 1;
-        }
-        acc = wave_sum(acc);
-        const bool any_bad = __any(bad);
-        if (lane == 0) xfer[q] = any_bad ? -1 : acc;
-        __syncthreads();
-    }
-
-    if (lane < np) {
-        const long p = p0 + lane;
-        const int rt = xfer[lane];
-        if (rt < 0) {
-            hcv_out[p] = -1; scv_out[p] = -1; feas_out[p] = 0; pen_out[p] = -1;
+        // ---- stage slot rows + sentinel column
+        const uint8_t* src = slot + p0 * E;
+        if ((E & 3) == 0) {
+            const int wpr = E >> 2;
+            const uint32_t* s32 = (const uint32_t*)src;
+            for (int w = threadIdx.x; w < np * wpr; w += nthr) {
+                const int r = w / wpr, c = w - r * wpr;
+                *(uint32_t*)(tile + r * SP + 4 * c) = s32[w];
+            }
         } else {
-            const int h = rt + corr;
-            const int sc = last + cons + single;
-            hcv_out[p] = h;
-            scv_out[p] = sc;
-            feas_out[p] = h == 0 ? 1 : 0;
-            pen_out[p] = h == 0 ? sc : 1000000 + h;
+            for (int b = threadIdx.x; b < np * E; b += nthr) {
+                const int r = b / E, c = b - r * E;
+                tile[r * SP + c] = src[b];
+            }
+        }
+        if (threadIdx.x < 64) tile[threadIdx.x * SP + E] = 63;
+        __syncthreads();
+
+        // ---- lane phase: per-student attendance masks (Solution.cpp:98-137)
+        {
+            const uint8_t* my = tile + lane * SP;
+            int sc = 0;
+            for (int st = wv; st < S; st += kTileWaves) {
+                const int k0 = pb.stc_off[st], k1 = pb.stc_off[st + 1];
+                uint64_t m = 0;
+                for (int k = k0; k < k1; k += 8) {
+                    int ev[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) ev[j] = pb.stc_ev[k + j];
+                    uint32_t sl[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) sl[j] = my[ev[j]];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) m |= 1ull << (sl[j] & 63);
+                }
+                sc += __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);
+#pragma unroll
+                for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);
+            }
+            part[wv * 64 + lane] = sc;
+        }
+
+        // ---- wave phase: hcv terms + last-slot term, one individual per wave at a time
+        for (int q = wv; q < np; q += kTileWaves) {
+            for (int c = lane; c < kSlots * EW64; c += 64) B[c] = 0ull;
+            for (int c = lane; c < kSlots * R; c += 64) cnt[c] = 0u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint8_t* rs = tile + q * SP;
+            const uint8_t* rr = room + (p0 + q) * E;
+            int h = 0, last = 0;
+            bool bad = false;
+            for (int e = lane; e < E; e += 64) {
+                const int s = rs[e], r = rr[e];
+                if (s >= kSlots || r >= R) { bad = true; continue; }
+                atomicOr((unsigned long long*)&B[s * EW64 + (e >> 6)], 1ull << (e & 63));
+                h += (int)atomicAdd(&cnt[s * R + r], 1u);                 // Solution.cpp:148-150
+                h += (int)(((pb.poss[e] >> r) & 1ull) ^ 1ull);             // :155-156
+                last += pb.sn[e] * (int)((kLastSlotMask >> s) & 1ull);     // :93-96
+            }
+            const bool any_bad = __any(bad);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (!any_bad) {
+                for (int i = lane; i < E; i += 64) {                       // :151-153
+                    const uint64_t* brow = B + rs[i] * EW64;
+                    for (int w = i >> 6; w < EW64; ++w) h += __popcll(pb.cupT[(size_t)w * E + i] & brow[w]);
+                }
+            }
+            h = wave_sum(h);
+            last = wave_sum(last);
+            if (lane == 0) { hq[q] = any_bad ? -1 : h; sq[q] = last; }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        __syncthreads();
+        if (wv == 0 && lane < np) {
+            const long p = p0 + lane;
+            const int h = hq[lane];
+            if (h < 0) {
+                hcv_out[p] = -1; scv_out[p] = -1; feas_out[p] = 0; pen_out[p] = -1;
+            } else {
+                int sc = sq[lane];
+#pragma unroll
+                for (int w = 0; w < kTileWaves; ++w) sc += part[w * 64 + lane];
+                hcv_out[p] = h;
+                scv_out[p] = sc;
+                feas_out[p] = h == 0 ? 1 : 0;
+                pen_out[p] = h == 0 ? sc : 1000000 + h;
+            }
         }
     }
 }
@@ -222,16 +272,6 @@ __global__ __launch_bounds__(kBlockThreads) void eval_block_kernel(DevProblem pb
     }
 }
 
-static int lane_stride(int E) {
-    int sp = (E + 3) & ~3;           // dword-aligned rows
-    if (((sp >> 2) & 1) == 0) sp += 4;  // odd dword count: conflict-free column reads
-    return sp;
-}
-
-static size_t lanes_lds_bytes(int E, int R) {
-    return (size_t)64 * lane_stride(E) + 4 * (size_t)((kSlots * R + 3) & ~3) + 64 * 4;
-}
-
 static size_t block_lds_bytes(int E, int R) {
     return 4 * (size_t)(kSlots * R + 3 * kSlots + 4) + 2 * (size_t)((E + 1) & ~1) + (size_t)E;
 }
@@ -251,13 +291,15 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     const int E = p->E, R = p->R;
-    const size_t lanes_lds = lanes_lds_bytes(E, R);
-    if (variant == 0) variant = (E <= 1024 && lanes_lds <= 65536) ? 1 : 2;
+    const TileLayout TL = tile_layout(E, R);
+    if (variant == 0) variant = (E <= 1024 && TL.bytes <= 80 * 1024) ? 1 : 2;
     if (variant == 1) {
-        if (lanes_lds > 160 * 1024) { set_error("instance too large for the lane kernel"); return TT_ERR_LIMIT; }
-        const int blocks = (P + 63) / 64;
-        hipLaunchKernelGGL(eval_lanes_kernel, dim3(blocks), dim3(64), lanes_lds, st, p->dev, slot, room, P,
-                           lane_stride(E), hcv, scv, feasible, penalty);
+        if (TL.bytes > 160 * 1024) { set_error("instance too large for the tile kernel"); return TT_ERR_LIMIT; }
+        const int tiles = (P + 63) / 64;
+        const int per_cu = TL.bytes <= 80 * 1024 ? 2 : 1;
+        const int grid = std::min(tiles, per_cu * p->num_cus);
+        hipLaunchKernelGGL(eval_tile_kernel, dim3(grid), dim3(64 * kTileWaves), TL.bytes, st, p->dev, slot, room, P,
+                           hcv, scv, feasible, penalty);
     } else {
         const size_t lds = block_lds_bytes(E, R);
         if (lds > 160 * 1024) { set_error("instance too large for the block kernel"); return TT_ERR_LIMIT; }

@@ -9,7 +9,7 @@
 #include "tt_common.h"
 
 struct tt_problem {
-    int E, R, F, S, device;
+    int E, R, F, S, device, num_cus;
     // host copies (tt_problem_derived, validation)
     std::vector<int32_t> student_number;
     std::vector<uint64_t> poss_bits;

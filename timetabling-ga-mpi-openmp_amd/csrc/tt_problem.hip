@@ -95,6 +95,22 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
             if (p->corr_bits[(size_t)i * EW + (j >> 5)] >> (j & 31) & 1u) cp_j.push_back(j);
         cp_off[i + 1] = (int32_t)cp_j.size();
     }
+    // word-major upper-triangle correlation bits for the bitset hcv term, and
+    // 8-padded per-student lists for the lane-per-individual attendance masks
+    const int EW64 = (E + 63) / 64;
+    std::vector<uint64_t> cupT((size_t)EW64 * E, 0ull);
+    for (int i = 0; i < E; i++)
+        for (int k = cp_off[i]; k < cp_off[i + 1]; k++) {
+            const int j = cp_j[k];
+            cupT[(size_t)(j >> 6) * E + i] |= 1ull << (j & 63);
+        }
+    std::vector<int32_t> stc_off(S + 1, 0), stc_ev;
+    for (int s = 0; s < S; s++) {
+        for (int k = stu_off[s]; k < stu_off[s + 1]; k++) stc_ev.push_back(stu_ev[k]);
+        while (stc_ev.size() % 8) stc_ev.push_back(E);
+        stc_off[s + 1] = (int32_t)stc_ev.size();
+    }
+    if (stc_ev.empty()) stc_ev.assign(8, E);
     // possibleRooms (Problem.cpp:130-148): size fits and every required feature present.
     p->poss_bits.assign(E, 0ull);
     for (int i = 0; i < E; i++)
@@ -121,6 +137,9 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         {cp_off.data(), sizeof(int32_t) * (E + 1), 0},
         {cp_j.data(), sizeof(int32_t) * cp_j.size(), 0},
         {nullptr, sizeof(int32_t) * 4, 0},   // status word
+        {cupT.data(), sizeof(uint64_t) * cupT.size(), 0},
+        {stc_off.data(), sizeof(int32_t) * stc_off.size(), 0},
+        {stc_ev.data(), sizeof(int32_t) * stc_ev.size(), 0},
     };
     size_t total = 0;
     for (auto& q : parts) { q.off = total; total += (q.bytes + 255) & ~(size_t)255; }
@@ -129,6 +148,7 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     int prev = 0;
     hipError_t he = hipGetDevice(&prev);
     if (he == hipSuccess) he = hipSetDevice(device);
+    if (he == hipSuccess) he = hipDeviceGetAttribute(&p->num_cus, hipDeviceAttributeMultiprocessorCount, device);
     if (he == hipSuccess) he = hipMalloc(&p->dev_block, total);
     if (he != hipSuccess) { check_hip(he, "tt_problem_create"); delete p; return TT_ERR_DEVICE; }
     std::vector<uint8_t> staging(total, 0);
@@ -151,6 +171,10 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     d.cp_off = (const int32_t*)(base + parts[7].off);
     d.cp_j = (const int32_t*)(base + parts[8].off);
     d.status = (int32_t*)(base + parts[9].off);
+    d.EW64 = EW64;
+    d.cupT = (const uint64_t*)(base + parts[10].off);
+    d.stc_off = (const int32_t*)(base + parts[11].off);
+    d.stc_ev = (const int32_t*)(base + parts[12].off);
     *out = p;
     return TT_OK;
 }
