@@ -178,3 +178,41 @@ def test_syn_scale_instance(orc):
     exp = o.eval(slots[idx], r_np)
     for x, e in zip((hcv, scv, feas, pen), exp):
         assert np.array_equal(x[idx], e)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_local_search_golden(problems, name):
+    """Solution::localSearch replayed on the GPU: phase 1 from random init
+    (200 steps), chained to 1000 and 2000 steps (phase 2 once feasible), and a
+    Move3-enabled run (prob3 = 1) — slots, rooms and final RNG state exact."""
+    dp, inst, z = problems[name]
+    n = z["ls_seeds"].size
+    s, r, g = dev(z["init_slots"][:n]), dev(z["init_rooms"][:n]), dev(z["ls_seeds"])
+    for steps, tag in ((200, "ls"), (1000, "ls2"), (2000, "ls3")):
+        dp.local_search(s, r, g, steps)
+        assert np.array_equal(host(s), z[f"{tag}_slots"]), tag
+        assert np.array_equal(host(r), z[f"{tag}_rooms"]), tag
+        assert np.array_equal(host(g), z[f"{tag}_rng"]), tag
+    s, r = dev(z["init_slots"][:4]), dev(z["init_rooms"][:4])
+    g = dev(ttga.population_seeds(9500, 4))
+    dp.local_search(s, r, g, 60, 1.0, 1.0, 1.0)
+    assert np.array_equal(host(s), z["lsp3_slots"]) and np.array_equal(host(r), z["lsp3_rooms"])
+    assert np.array_equal(host(g), z["lsp3_rng"])
+    assert dp.status() == 0
+
+
+def test_local_search_random_vs_oracle(orc):
+    inst = ttga.generate(180, 7, 4, 140, seed=17)
+    dp = native.DeviceProblem(inst)
+    o = orc.problem(inst)
+    P = 24
+    s0, r0, _ = o.random_init(ttga.population_seeds(606, P))
+    seeds = ttga.population_seeds(707, P)
+    s, r, g = dev(s0), dev(r0), dev(seeds)
+    dp.local_search(s, r, g, 500)
+    es, er, eg = o.local_search(s0, r0, seeds, 500)
+    assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg)
+    # chained into phase 2
+    dp.local_search(s, r, g, 3000)
+    es, er, eg = o.local_search(es, er, eg, 3000)
+    assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg)

@@ -30,6 +30,7 @@ struct DevProblem {
     int EW64;                     // 64-bit words per event bitset
     const uint64_t* cupT;         // [EW64][E] upper-triangle correlation bits, word-major:
                                   //   cupT[w*E+i] bit b <=> corr(i, 64w+b) and 64w+b > i
+    const uint64_t* corr64;       // [E][EW64] full eventCorrelations rows (diagonal included)
     const int32_t* stc_off;       // [S+1] per-student event lists padded to multiples of 8
     const int32_t* stc_ev;        //   padding entries hold E (a sentinel column)
     int32_t* status;              // device status word (tt_device_status)

@@ -60,16 +60,24 @@ __host__ __device__ inline TileLayout tile_layout(int E, int R) {
     return L;
 }
 
+// EWC > 0: compile-time number of 64-event words (E <= 64*EWC); the per-event
+// invariants of a lane's events (possible rooms, studentNumber, the upper-
+// triangle correlation words) live in registers for the whole launch, so an
+// individual costs only its own slot/room reads plus LDS traffic.
+// EWC == 0: runtime word count, invariants re-read from global memory.
+template <int EWC>
 __global__ __launch_bounds__(64 * kTileWaves) void eval_tile_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
                                                                      const uint8_t* __restrict__ room, int P,
                                                                      int32_t* __restrict__ hcv_out,
                                                                      int32_t* __restrict__ scv_out,
                                                                      uint8_t* __restrict__ feas_out,
-                                                                     int32_t* __restrict__ pen_out) {
+                                                                     int32_t* __restrict__ pen_out, int ablate) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int E = pb.E, R = pb.R, S = pb.S, EW64 = pb.EW64;
+    const int E = pb.E, R = pb.R, S = pb.S;
+    const int EW64 = EWC > 0 ? EWC : pb.EW64;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const TileLayout L = tile_layout(E, R);
+    // ablate (profiling only, results invalid): 1 skip lane phase, 2 skip wave phase, 4 skip corr words
     const int SP = L.SP;
     uint8_t* tile = lds;
     uint64_t* B = (uint64_t*)(lds + L.off_wave + (size_t)wv * L.WS);   // [45][EW64]
@@ -79,6 +87,21 @@ __global__ __launch_bounds__(64 * kTileWaves) void eval_tile_kernel(DevProblem p
     int32_t* sq = hq + 64;                                              // [64]
     const int tiles = (P + 63) / 64;
     const int nthr = 64 * kTileWaves;
+
+    constexpr int NR = EWC > 0 ? EWC : 1;
+    uint64_t inv_poss[NR], inv_cup[NR][NR];
+    int inv_sn[NR];
+    if constexpr (EWC > 0) {
+#pragma unroll
+        for (int r = 0; r < EWC; ++r) {
+            const int e = lane + 64 * r;
+            const bool ok = e < E;
+            inv_poss[r] = ok ? pb.poss[e] : ~0ull;
+            inv_sn[r] = ok ? pb.sn[e] : 0;
+#pragma unroll
+            for (int w = 0; w < EWC; ++w) inv_cup[r][w] = (w >= r && ok) ? pb.cupT[(size_t)w * E + e] : 0ull;
+        }
+    }
 
     for (int tl = blockIdx.x; tl < tiles; tl += gridDim.x) {
         const long p0 = (long)tl * 64;
@@ -103,7 +126,7 @@ __global__ __launch_bounds__(64 * kTileWaves) void eval_tile_kernel(DevProblem p
         __syncthreads();
 
         // ---- lane phase: per-student attendance masks (Solution.cpp:98-137)
-        {
+        if (!(ablate & 1)) {
             const uint8_t* my = tile + lane * SP;
             int sc = 0;
             for (int st = wv; st < S; st += kTileWaves) {
@@ -127,7 +150,7 @@ __global__ __launch_bounds__(64 * kTileWaves) void eval_tile_kernel(DevProblem p
         }
 
         // ---- wave phase: hcv terms + last-slot term, one individual per wave at a time
-        for (int q = wv; q < np; q += kTileWaves) {
+        for (int q = wv; q < ((ablate & 2) ? 0 : np); q += kTileWaves) {
             for (int c = lane; c < kSlots * EW64; c += 64) B[c] = 0ull;
             for (int c = lane; c < kSlots * R; c += 64) cnt[c] = 0u;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -137,27 +160,67 @@ __global__ __launch_bounds__(64 * kTileWaves) void eval_tile_kernel(DevProblem p
             const uint8_t* rr = room + (p0 + q) * E;
             int h = 0, last = 0;
             bool bad = false;
-            for (int e = lane; e < E; e += 64) {
-                const int s = rs[e], r = rr[e];
-                if (s >= kSlots || r >= R) { bad = true; continue; }
-                atomicOr((unsigned long long*)&B[s * EW64 + (e >> 6)], 1ull << (e & 63));
-                h += (int)atomicAdd(&cnt[s * R + r], 1u);                 // Solution.cpp:148-150
-                h += (int)(((pb.poss[e] >> r) & 1ull) ^ 1ull);             // :155-156
-                last += pb.sn[e] * (int)((kLastSlotMask >> s) & 1ull);     // :93-96
-            }
-            const bool any_bad = __any(bad);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (!any_bad) {
-                for (int i = lane; i < E; i += 64) {                       // :151-153
-                    const uint64_t* brow = B + rs[i] * EW64;
-                    for (int w = i >> 6; w < EW64; ++w) h += __popcll(pb.cupT[(size_t)w * E + i] & brow[w]);
+            if constexpr (EWC > 0) {
+                uint32_t sv[EWC], rv[EWC];
+#pragma unroll
+                for (int r = 0; r < EWC; ++r) {
+                    const int e = lane + 64 * r;
+                    sv[r] = e < E ? rs[e] : 0u;
+                    rv[r] = e < E ? rr[e] : 0u;
                 }
+#pragma unroll
+                for (int r = 0; r < EWC; ++r) {
+                    if (lane + 64 * r < E) {
+                        const int s = sv[r], ro = rv[r];
+                        if (s >= kSlots || ro >= R) {
+                            bad = true;
+                        } else {
+                            atomicOr((unsigned long long*)&B[s * EWC + r], 1ull << lane);
+                            h += (int)atomicAdd(&cnt[s * R + ro], 1u);                 // Solution.cpp:148-150
+                            h += (int)(((inv_poss[r] >> ro) & 1ull) ^ 1ull);            // :155-156
+                            last += inv_sn[r] * (int)((kLastSlotMask >> s) & 1ull);     // :93-96
+                        }
+                    }
+                }
+                const bool any_bad = __any(bad);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (!any_bad && !(ablate & 4)) {
+#pragma unroll
+                    for (int r = 0; r < EWC; ++r) {                                     // :151-153
+                        if (lane + 64 * r < E) {
+                            const uint64_t* brow = B + sv[r] * EWC;
+#pragma unroll
+                            for (int w = r; w < EWC; ++w) h += __popcll(inv_cup[r][w] & brow[w]);
+                        }
+                    }
+                }
+                bad = any_bad;
+            } else {
+                for (int e = lane; e < E; e += 64) {
+                    const int s = rs[e], r = rr[e];
+                    if (s >= kSlots || r >= R) { bad = true; continue; }
+                    atomicOr((unsigned long long*)&B[s * EW64 + (e >> 6)], 1ull << (e & 63));
+                    h += (int)atomicAdd(&cnt[s * R + r], 1u);
+                    h += (int)(((pb.poss[e] >> r) & 1ull) ^ 1ull);
+                    last += pb.sn[e] * (int)((kLastSlotMask >> s) & 1ull);
+                }
+                const bool any_bad = __any(bad);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (!any_bad && !(ablate & 4)) {
+                    for (int i = lane; i < E; i += 64) {
+                        const uint64_t* brow = B + rs[i] * EW64;
+                        for (int w = i >> 6; w < EW64; ++w) h += __popcll(pb.cupT[(size_t)w * E + i] & brow[w]);
+                    }
+                }
+                bad = any_bad;
             }
             h = wave_sum(h);
             last = wave_sum(last);
-            if (lane == 0) { hq[q] = any_bad ? -1 : h; sq[q] = last; }
+            if (lane == 0) { hq[q] = bad ? -1 : h; sq[q] = last; }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -285,6 +348,8 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
     int rc = check_pop_args(p, P, slot, room);
     if (rc) return rc;
     if (P > 0 && (!hcv || !scv || !feasible || !penalty)) { set_error("null output buffer"); return TT_ERR_INVALID; }
+    const int ablate = variant >> 4;   // profiling-only phase switches (tile kernel)
+    variant &= 15;
     if (variant < 0 || variant > 2) { set_error("unknown eval variant"); return TT_ERR_INVALID; }
     if (P == 0) return TT_OK;
     rc = use_device(p);
@@ -296,10 +361,26 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
     if (variant == 1) {
         if (TL.bytes > 160 * 1024) { set_error("instance too large for the tile kernel"); return TT_ERR_LIMIT; }
         const int tiles = (P + 63) / 64;
-        const int per_cu = TL.bytes <= 80 * 1024 ? 2 : 1;
-        const int grid = std::min(tiles, per_cu * p->num_cus);
-        hipLaunchKernelGGL(eval_tile_kernel, dim3(grid), dim3(64 * kTileWaves), TL.bytes, st, p->dev, slot, room, P,
-                           hcv, scv, feasible, penalty);
+        const dim3 b(64 * kTileWaves);
+        auto launch = [&](auto kern) -> int {
+            int per_cu = 0;
+            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, b.x, TL.bytes));
+            const int grid = std::min(tiles, std::max(1, per_cu) * p->num_cus);
+            hipLaunchKernelGGL(kern, dim3(grid), b, TL.bytes, st, p->dev, slot, room, P, hcv, scv, feasible, penalty,
+                               ablate);
+            return TT_OK;
+        };
+        switch (p->dev.EW64) {
+            case 1: rc = launch(eval_tile_kernel<1>); break;
+            case 2: rc = launch(eval_tile_kernel<2>); break;
+            case 3: rc = launch(eval_tile_kernel<3>); break;
+            case 4: rc = launch(eval_tile_kernel<4>); break;
+            case 5: rc = launch(eval_tile_kernel<5>); break;
+            case 6: rc = launch(eval_tile_kernel<6>); break;
+            case 7: rc = launch(eval_tile_kernel<7>); break;
+            default: rc = launch(eval_tile_kernel<0>); break;
+        }
+        if (rc) return rc;
     } else {
         const size_t lds = block_lds_bytes(E, R);
         if (lds > 160 * 1024) { set_error("instance too large for the block kernel"); return TT_ERR_LIMIT; }

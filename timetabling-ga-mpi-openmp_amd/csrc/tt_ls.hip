@@ -1,12 +1,550 @@
-// Solution::localSearch (Solution.cpp:471-769) — device implementation pending.
+// Batched Solution::localSearch (Solution.cpp:471-769): one WAVE per
+// individual, every individual with its own Park-Miller stream, bit-exact with
+// the reference (same RNG draws, same first-improvement acceptance, same step
+// budget shared by both phases).
+//
+// State of an individual, in LDS: slot and room of every event, per-slot event
+// bitsets B[t] (the ascending timeslot_events lists), the room histogram of
+// every slot and its room-clash pair count. A trial move (Move1/2/3,
+// Solution.cpp:357-439) is never materialised as a copied Solution: the
+// neighbour is the current state plus <=3 moved events; its <=3 touched slots
+// get new bitsets NB[k] and are re-matched IN PARALLEL, one lane per slot
+// (the assignRooms replay of tt_match.h), writing the neighbour's rooms into a
+// mirror row nrr[]. The delta evaluators then read:
+//   eventAffectedHcv(e)        = roomPairs(slot) + popcount(corr(e) & set) - corr(e,e)
+//   affectedRoomInTimeslotHcv  = roomPairs(slot)
+//   eventHcv(e)                = hist[slot][room(e)] - 1 + popcount(corr(e) & B) - corr(e,e)
+//   eventScv / singleClassesScv from each student's 45-bit attendance mask
+//                                (lanes = students of e, Solution.cpp:248-355)
+// Accept copies the touched slots into the current state; reject restores nrr.
 #include "tt_internal.h"
+#include "tt_match.h"
+
+namespace ttga {
+
+constexpr int kLsTasks = 3;
+
+struct LsLayout {
+    size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, task;
+    size_t task_bytes;
+    int NT;              // events per matcher task (min(E, 256))
+    size_t bytes;
+};
+
+__host__ __device__ inline LsLayout ls_layout(int E, int R, int EW) {
+    LsLayout L;
+    size_t b = 0;
+    auto al = [&](size_t a) { b = (b + a - 1) & ~(a - 1); };
+    L.sl = b; b += E + 1;
+    L.rr = b; b += E;
+    L.nrr = b; b += E;
+    al(2); L.evl = b; b += 2 * (size_t)E;
+    al(8); L.B = b; b += 8 * (size_t)kSlots * EW;
+    L.NB = b; b += 8 * (size_t)kLsTasks * EW;
+    L.rp = b; b += 4 * (size_t)kSlots;
+    L.hist = b; b += 2 * (size_t)kSlots * R;
+    al(4); L.misc = b; b += 4 * 32;
+    L.NT = E < kMaxSlotEvents ? E : kMaxSlotEvents;
+    size_t tb = 11 * (size_t)L.NT + 1 + 4 * (size_t)R;   // pl, ev, mr, (pad), hist, rm, dr
+    L.task_bytes = (tb + 15) & ~(size_t)15;
+    al(16); L.task = b; b += kLsTasks * L.task_bytes;
+    L.bytes = (b + 15) & ~(size_t)15;
+    return L;
+}
+
+struct LsTask {
+    uint64_t* pl;
+    uint16_t* ev;
+    uint8_t* mr;
+    uint8_t* rm;
+    uint8_t* dr;
+    uint16_t* hist;
+};
+
+struct LsState;
+__device__ __forceinline__ LsTask get_task(const LsState& S, int k);
+
+struct LsState {
+    DevProblem pb;
+    int E, R, EW, lane;
+    uint8_t *sl, *rr, *nrr;
+    uint16_t* evl;
+    uint64_t *B, *NB;
+    int32_t* rp;
+    uint16_t* hist;
+    int32_t* misc;       // [0..2] neighbour room pairs per task
+    uint8_t* task_base;
+    int task_bytes, NT;
+    // neighbour description (wave-uniform)
+    int nmv, mv_e[3], mv_t[3];
+    int nts, ts[3];
+};
+
+__device__ __forceinline__ LsTask get_task(const LsState& S, int k) {
+    uint8_t* tb = S.task_base + (size_t)k * S.task_bytes;
+    LsTask T;
+    T.pl = (uint64_t*)tb;
+    T.ev = (uint16_t*)(tb + 8 * (size_t)S.NT);
+    T.mr = tb + 10 * (size_t)S.NT;
+    T.hist = (uint16_t*)(tb + ((11 * (size_t)S.NT + 1) & ~(size_t)1));
+    T.rm = (uint8_t*)(T.hist + S.R);
+    T.dr = T.rm + S.R;
+    return T;
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int slot_nb(const LsState& S, int j) {
+    int s = S.sl[j];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (k < S.nmv && j == S.mv_e[k]) s = S.mv_t[k];
+    return s;
+}
+
+// sum over words of popcount(corr64[e] & set[w]) - corr(e,e)  (the "i != e" of the reference)
+__device__ __forceinline__ int corr_in_set(const LsState& S, int e, const uint64_t* set) {
+    int c = 0;
+    for (int w = S.lane; w < S.EW; w += 64) c += __popcll(S.pb.corr64[(size_t)e * S.EW + w] & set[w]);
+    c = wave_sum(c);
+    const int self = (int)((S.pb.corr64[(size_t)e * S.EW + (e >> 6)] >> (e & 63)) & 1ull);
+    return c - self;
+}
+
+// eventAffectedHcv(e) (Solution.cpp:194-215) in the current state
+__device__ __forceinline__ int eah_cur(const LsState& S, int e) {
+    const int t = S.sl[e];
+    return S.rp[t] + corr_in_set(S, e, S.B + (size_t)t * S.EW);
+}
+
+__device__ __forceinline__ int task_of(const LsState& S, int t) {
+    int k = 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+        if (q < S.nts && S.ts[q] == t) k = q;
+    return k;
+}
+
+// eventAffectedHcv(e) in the neighbour
+__device__ __forceinline__ int eah_nb(const LsState& S, int e) {
+    const int k = task_of(S, slot_nb(S, e));
+    return S.misc[k] + corr_in_set(S, e, S.NB + (size_t)k * S.EW);
+}
+
+// eventHcv(e) (Solution.cpp:173-191) in the current state
+__device__ __forceinline__ int ehcv_cur(const LsState& S, int e) {
+    const int t = S.sl[e];
+    return (int)S.hist[t * S.R + S.rr[e]] - 1 + corr_in_set(S, e, S.B + (size_t)t * S.EW);
+}
+
+// eventScv(e) and singleClassesScv(e) (Solution.cpp:248-355) in the current
+// (nb = false) or neighbour (nb = true) state.
+__device__ __forceinline__ void scv_terms(const LsState& S, int e, bool nb, int& es, int& scs) {
+    const DevProblem& pb = S.pb;
+    const int t = nb ? slot_nb(S, e) : S.sl[e];
+    const int day = t / 9, pos = t - 9 * day;
+    const int k0 = pb.ev_off[e], k1 = pb.ev_off[e + 1];
+    int a = 0, b = 0;
+    for (int k = k0 + S.lane; k < k1; k += 64) {
+        const int st = pb.ev_stu[k];
+        uint64_t m = 0;
+        const int c0 = pb.stc_off[st], c1 = pb.stc_off[st + 1];
+        for (int c = c0; c < c1; c += 8) {
+            int ev[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ev[j] = pb.stc_ev[c + j];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m |= 1ull << ((nb ? slot_nb(S, ev[j]) : S.sl[ev[j]]) & 63);
+        }
+        const uint32_t dm = (uint32_t)(m >> (9 * day)) & 0x1FFu;
+        const uint32_t others = dm & ~(1u << pos);
+        auto at = [&](int x) -> int { return (int)((dm >> x) & 1u); };
+        if (pos < 8 && at(pos + 1)) a += (pos < 7 ? at(pos + 2) : 0) + (pos > 0 ? at(pos - 1) : 0);
+        if (pos > 1) a += at(pos - 1) & at(pos - 2);
+        a += others == 0u;
+        b += __popc(others) == 1;
+    }
+    es = wave_sum(a) + (pos == 8 ? pb.sn[e] : 0);
+    scs = wave_sum(b);
+}
+
+// Builds NB[k] for the touched slots and re-matches them, one lane per slot.
+__device__ __forceinline__ void build_and_match(LsState& S) {
+    const int EW = S.EW;
+    for (int k = 0; k < S.nts; ++k) {
+        const int t = S.ts[k];
+        for (int w = S.lane; w < EW; w += 64) {
+            uint64_t x = S.B[(size_t)t * EW + w];
+            for (int q = 0; q < S.nmv; ++q) {
+                const int e = S.mv_e[q];
+                if (S.sl[e] == t && (e >> 6) == w) x &= ~(1ull << (e & 63));
+            }
+            for (int q = 0; q < S.nmv; ++q) {
+                const int e = S.mv_e[q];
+                if (S.mv_t[q] == t && (e >> 6) == w) x |= 1ull << (e & 63);
+            }
+            S.NB[(size_t)k * EW + w] = x;
+        }
+    }
+    wave_sync();
+    if (S.lane < S.nts) {
+        const int k = S.lane;
+        const LsTask T = get_task(S, k);
+        const uint64_t* nb = S.NB + (size_t)k * EW;
+        int N = 0;
+        bool over = false;
+        for (int w = 0; w < EW; ++w) {
+            uint64_t x = nb[w];
+            while (x) {
+                const int e = 64 * w + __builtin_ctzll(x);
+                x &= x - 1;
+                if (N < kMaxSlotEvents) { T.ev[N] = (uint16_t)e; T.pl[N] = S.pb.poss[e]; }
+                else over = true;
+                ++N;
+            }
+        }
+        for (int r = 0; r < S.R; ++r) T.hist[r] = 0;
+        int pairs = 0;
+        if (over) {
+            atomicOr(S.pb.status, 1);
+            for (int i = 0; i < kMaxSlotEvents; ++i) S.nrr[T.ev[i]] = 0xFF;
+        } else if (N > 0) {
+            if (N <= 64) match_slot<1>(S.R, T.ev, T.pl, N, T.mr, T.rm, T.dr, S.nrr);
+            else match_slot<4>(S.R, T.ev, T.pl, N, T.mr, T.rm, T.dr, S.nrr);
+            for (int i = 0; i < N; ++i) {
+                const int r = S.nrr[T.ev[i]];
+                pairs += T.hist[r];
+                T.hist[r] = (uint16_t)(T.hist[r] + 1);
+            }
+        }
+        S.misc[k] = pairs;
+    }
+    wave_sync();
+}
+
+// events of neighbour slot k: copy rooms between rr and nrr
+__device__ __forceinline__ void sync_rooms(LsState& S, bool accept) {
+    for (int k = 0; k < S.nts; ++k) {
+        const uint64_t* nb = S.NB + (size_t)k * S.EW;
+        for (int w = S.lane; w < S.EW; w += 64) {
+            uint64_t x = nb[w];
+            while (x) {
+                const int e = 64 * w + __builtin_ctzll(x);
+                x &= x - 1;
+                if (accept) S.rr[e] = S.nrr[e];
+                else S.nrr[e] = S.rr[e];
+            }
+        }
+    }
+    wave_sync();
+}
+
+__device__ __forceinline__ void accept(LsState& S) {
+    sync_rooms(S, true);
+    for (int k = 0; k < S.nts; ++k) {
+        const int t = S.ts[k];
+        for (int w = S.lane; w < S.EW; w += 64) S.B[(size_t)t * S.EW + w] = S.NB[(size_t)k * S.EW + w];
+        const LsTask T = get_task(S, k);
+        for (int r = S.lane; r < S.R; r += 64) S.hist[t * S.R + r] = T.hist[r];
+    }
+    if (S.lane == 0) {
+        for (int k = 0; k < S.nts; ++k) S.rp[S.ts[k]] = S.misc[k];
+        for (int q = 0; q < S.nmv; ++q) S.sl[S.mv_e[q]] = (uint8_t)S.mv_t[q];
+    }
+    wave_sync();
+}
+
+__device__ __forceinline__ void add_touched(LsState& S, int t) {
+    const bool seen = (S.nts > 0 && S.ts[0] == t) || (S.nts > 1 && S.ts[1] == t) || (S.nts > 2 && S.ts[2] == t);
+    if (seen) return;
+    if (S.nts == 0) S.ts[0] = t;
+    else if (S.nts == 1) S.ts[1] = t;
+    else S.ts[2] = t;
+    S.nts++;
+}
+
+__device__ __forceinline__ void set_move(LsState& S, int type, int e1, int a2, int e3) {
+    // type 1: e1 -> slot a2; type 2: swap e1, a2; type 3: e1->slot(a2), a2->slot(e3), e3->slot(e1)
+    S.nts = 0;
+    if (type == 1) {
+        S.nmv = 1; S.mv_e[0] = e1; S.mv_t[0] = a2;
+        add_touched(S, a2); add_touched(S, S.sl[e1]);
+    } else if (type == 2) {
+        const int t1 = S.sl[e1], t2 = S.sl[a2];
+        S.nmv = 2; S.mv_e[0] = e1; S.mv_t[0] = t2; S.mv_e[1] = a2; S.mv_t[1] = t1;
+        add_touched(S, t2); add_touched(S, t1);
+    } else {
+        const int t1 = S.sl[e1], t2 = S.sl[a2], t3 = S.sl[e3];
+        S.nmv = 3; S.mv_e[0] = e1; S.mv_t[0] = t2; S.mv_e[1] = a2; S.mv_t[1] = t3; S.mv_e[2] = e3; S.mv_t[2] = t1;
+        add_touched(S, t2); add_touched(S, t3); add_touched(S, t1);
+    }
+}
+
+// whole-solution feasibility (Solution.cpp:63-84) from the incremental state
+__device__ __forceinline__ bool feasible_now(const LsState& S) {
+    int h = 0;
+    for (int t = S.lane; t < kSlots; t += 64) h += S.rp[t];
+    for (int e = S.lane; e < S.E; e += 64) {
+        const int t = S.sl[e];
+        int c = 0;
+        for (int w = 0; w < S.EW; ++w) c += __popcll(S.pb.corr64[(size_t)e * S.EW + w] & S.B[(size_t)t * S.EW + w]);
+        c -= (int)((S.pb.corr64[(size_t)e * S.EW + (e >> 6)] >> (e & 63)) & 1ull);
+        h += c;   // every correlated same-slot pair is counted twice, only zero matters
+        h += (int)(((S.pb.poss[e] >> S.rr[e]) & 1ull) ^ 1ull);
+    }
+    return wave_sum(h) == 0;
+}
+
+__global__ __launch_bounds__(64) void local_search_kernel(DevProblem pb, uint8_t* __restrict__ slot,
+                                                          uint8_t* __restrict__ room, int64_t* __restrict__ rng,
+                                                          int P, int max_steps, double p1, double p2, double p3) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int E = pb.E, R = pb.R, EW = pb.EW64;
+    const int lane = threadIdx.x;
+    const long p = blockIdx.x;
+    const LsLayout L = ls_layout(E, R, EW);
+    LsState S;
+    S.pb = pb; S.E = E; S.R = R; S.EW = EW; S.lane = lane;
+    S.sl = lds + L.sl; S.rr = lds + L.rr; S.nrr = lds + L.nrr;
+    S.evl = (uint16_t*)(lds + L.evl);
+    S.B = (uint64_t*)(lds + L.B); S.NB = (uint64_t*)(lds + L.NB);
+    S.rp = (int32_t*)(lds + L.rp); S.hist = (uint16_t*)(lds + L.hist);
+    S.misc = (int32_t*)(lds + L.misc);
+    S.task_base = lds + L.task;
+    S.task_bytes = (int)L.task_bytes;
+    S.NT = L.NT;
+    S.nmv = 0; S.nts = 0;
+
+    // ---- load the individual, derive the incremental state
+    bool bad = false;
+    for (int e = lane; e < E; e += 64) {
+        const uint8_t s = slot[p * E + e], r = room[p * E + e];
+        bad |= s >= kSlots || r >= R;
+        S.sl[e] = s; S.rr[e] = r; S.nrr[e] = r; S.evl[e] = (uint16_t)e;
+    }
+    if (lane == 0) S.sl[E] = 63;
+    for (int c = lane; c < kSlots * EW; c += 64) S.B[c] = 0ull;
+    for (int c = lane; c < kSlots * R; c += 64) S.hist[c] = 0;
+    __syncthreads();
+    if (__any(bad)) {                       // invalid genome: leave it untouched
+        if (lane == 0) atomicOr(pb.status, 2);
+        return;
+    }
+    for (int e = lane; e < E; e += 64) {
+        const int s = S.sl[e];
+        atomicOr((unsigned long long*)&S.B[(size_t)s * EW + (e >> 6)], 1ull << (e & 63));
+    }
+    __syncthreads();
+    if (lane < kSlots) {                    // room histogram + clash pairs of every slot
+        int pairs = 0;
+        for (int w = 0; w < EW; ++w) {
+            uint64_t x = S.B[(size_t)lane * EW + w];
+            while (x) {
+                const int e = 64 * w + __builtin_ctzll(x);
+                x &= x - 1;
+                const int r = S.rr[e];
+                pairs += S.hist[lane * R + r];
+                S.hist[lane * R + r] = (uint16_t)(S.hist[lane * R + r] + 1);
+            }
+        }
+        S.rp[lane] = pairs;
+    }
+    __syncthreads();
+
+    int64_t st = rng[p];
+    // scramble the event list (Solution.cpp:476-484)
+    if (lane == 0) {
+        int64_t s2 = st;
+        for (int i = 0; i < E; ++i) {
+            const int j = pm_pick(s2, E);
+            const uint16_t h = S.evl[i];
+            S.evl[i] = S.evl[j];
+            S.evl[j] = h;
+        }
+    }
+    for (int i = 0; i < E; ++i) pm_next(st);    // every lane keeps the (uniform) stream
+    __syncthreads();
+
+    int step = 0, evc = 0;
+    bool better = false;
+    const long guard_max = 4l * (long)E * ((long)max_steps + 2) + 1024;
+    long guard = 0;
+    if (!feasible_now(S)) {                                             // phase 1 (Solution.cpp:497-618)
+        for (int i = 0; evc < E; i = (i + 1) % E) {
+            if (step > max_steps || ++guard > guard_max) break;
+            const int ei = S.evl[i];
+            if (ehcv_cur(S, ei) == 0) { evc++; continue; }
+            const int t_start = pm_pick(st, kSlots);
+            const int t_orig = S.sl[ei];
+            for (int h = 0, t = t_start; h < kSlots; t = (t + 1) % kSlots, h++) {
+                if (step > max_steps) break;
+                if (pm_next(st) < p1) {
+                    step++;
+                    set_move(S, 1, ei, t, 0);
+                    build_and_match(S);
+                    const int n = eah_nb(S, ei) + S.misc[task_of(S, t_orig)];
+                    const int c = eah_cur(S, ei) + S.rp[t];
+                    if (n < c) { accept(S); evc = 0; better = true; break; }
+                    sync_rooms(S, false);
+                }
+            }
+            if (better) { better = false; continue; }
+            if (p2 != 0) {
+                for (int j = (i + 1) % E; j != i; j = (j + 1) % E) {
+                    if (step > max_steps) break;
+                    if (pm_next(st) < p2) {
+                        step++;
+                        const int ej = S.evl[j];
+                        const int c = eah_cur(S, ei) + eah_cur(S, ej);
+                        set_move(S, 2, ei, ej, 0);
+                        build_and_match(S);
+                        const int n = eah_nb(S, ei) + eah_nb(S, ej);
+                        if (n < c) { accept(S); evc = 0; better = true; break; }
+                        sync_rooms(S, false);
+                    }
+                }
+                if (better) { better = false; continue; }
+            }
+            if (p3 != 0) {
+                for (int j = (i + 1) % E; j != i; j = (j + 1) % E) {
+                    if (step > max_steps) break;
+                    for (int k = (j + 1) % E; k != i; k = (k + 1) % E) {
+                        if (step > max_steps) break;
+                        const int ej = S.evl[j], ek = S.evl[k];
+                        if (pm_next(st) < p3) {
+                            step++;
+                            const int c = eah_cur(S, ei) + eah_cur(S, ej) + eah_cur(S, ek);
+                            set_move(S, 3, ei, ej, ek);
+                            build_and_match(S);
+                            const int n = eah_nb(S, ei) + eah_nb(S, ej) + eah_nb(S, ek);
+                            if (n < c) { accept(S); evc = 0; better = true; break; }
+                            sync_rooms(S, false);
+                        }
+                        if (step > max_steps) break;
+                        if (pm_next(st) < p3) {
+                            step++;
+                            const int c = eah_cur(S, ei) + eah_cur(S, ek) + eah_cur(S, ej);
+                            set_move(S, 3, ei, ek, ej);
+                            build_and_match(S);
+                            const int n = eah_nb(S, ei) + eah_nb(S, ek) + eah_nb(S, ej);
+                            if (n < c) { accept(S); evc = 0; better = true; break; }
+                            sync_rooms(S, false);
+                        }
+                    }
+                    if (better) break;
+                }
+                if (better) { better = false; continue; }
+            }
+            evc++;
+        }
+    }
+    if (feasible_now(S)) {                                              // phase 2 (Solution.cpp:619-768)
+        evc = 0;
+        for (int i = 0; evc < E; i = (i + 1) % E) {
+            if (step > max_steps || ++guard > guard_max) break;
+            const int ei = S.evl[i];
+            int cur, scs_i;
+            scv_terms(S, ei, false, cur, scs_i);
+            if (cur == 0) { evc++; continue; }
+            const int t_start = pm_pick(st, kSlots);
+            for (int h = 0, t = t_start; h < kSlots; t = (t + 1) % kSlots, h++) {
+                if (step > max_steps) break;
+                if (pm_next(st) < p1) {
+                    step++;
+                    set_move(S, 1, ei, t, 0);
+                    build_and_match(S);
+                    if (eah_nb(S, ei) == 0) {
+                        int es_n, scs_n;
+                        scv_terms(S, ei, true, es_n, scs_n);
+                        if (es_n + scs_i - scs_n < cur) { accept(S); evc = 0; better = true; break; }
+                    }
+                    sync_rooms(S, false);
+                }
+            }
+            if (better) { better = false; continue; }
+            if (p2 != 0) {
+                for (int j = (i + 1) % E; j != i; j = (j + 1) % E) {
+                    if (step > max_steps) break;
+                    if (pm_next(st) < p2) {
+                        step++;
+                        const int ej = S.evl[j];
+                        set_move(S, 2, ei, ej, 0);
+                        build_and_match(S);
+                        if (eah_nb(S, ei) + eah_nb(S, ej) == 0) {
+                            int es_ni, scs_ni, es_nj, scs_nj, es_cj, scs_cj;
+                            scv_terms(S, ei, true, es_ni, scs_ni);
+                            scv_terms(S, ej, true, es_nj, scs_nj);
+                            scv_terms(S, ej, false, es_cj, scs_cj);
+                            const int n = es_ni + scs_i - scs_ni + es_nj + scs_cj - scs_nj;
+                            if (n < cur + es_cj) { accept(S); evc = 0; better = true; break; }
+                        }
+                        sync_rooms(S, false);
+                    }
+                }
+                if (better) { better = false; continue; }
+            }
+            if (p3 != 0) {
+                for (int j = (i + 1) % E; j != i; j = (j + 1) % E) {
+                    if (step > max_steps) break;
+                    for (int k = (j + 1) % E; k != i; k = (k + 1) % E) {
+                        if (step > max_steps) break;
+                        const int ej = S.evl[j], ek = S.evl[k];
+                        for (int order = 0; order < 2; ++order) {
+                            if (order == 1 && step > max_steps) break;
+                            if (!(pm_next(st) < p3)) continue;
+                            step++;
+                            const int a = order ? ek : ej, b = order ? ej : ek;
+                            set_move(S, 3, ei, a, b);
+                            build_and_match(S);
+                            if (eah_nb(S, ei) + eah_nb(S, a) + eah_nb(S, b) == 0) {
+                                int es_ni, scs_ni, es_na, scs_na, es_nb, scs_nb, es_ca, scs_ca, es_cb, scs_cb;
+                                scv_terms(S, ei, true, es_ni, scs_ni);
+                                scv_terms(S, a, true, es_na, scs_na);
+                                scv_terms(S, b, true, es_nb, scs_nb);
+                                scv_terms(S, a, false, es_ca, scs_ca);
+                                scv_terms(S, b, false, es_cb, scs_cb);
+                                const int n = es_ni + scs_i - scs_ni + es_na + scs_ca - scs_na + es_nb + scs_cb - scs_nb;
+                                if (n < cur + es_ca + es_cb) { accept(S); evc = 0; better = true; break; }
+                            }
+                            sync_rooms(S, false);
+                        }
+                        if (better) break;
+                    }
+                    if (better) break;
+                }
+                if (better) { better = false; continue; }
+            }
+            evc++;
+        }
+    }
+    if (guard > guard_max && lane == 0) atomicOr(pb.status, 4);
+
+    __syncthreads();
+    for (int e = lane; e < E; e += 64) {
+        slot[p * E + e] = S.sl[e];
+        room[p * E + e] = S.rr[e];
+    }
+    if (lane == 0) rng[p] = st;
+}
+
+}  // namespace ttga
 
 using namespace ttga;
 
 extern "C" int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P,
                                int max_steps, double p1, double p2, double p3, void* stream) {
-    (void)slot; (void)room; (void)rng; (void)P; (void)max_steps; (void)p1; (void)p2; (void)p3; (void)stream;
-    if (!p) { set_error("null tt_problem"); return TT_ERR_INVALID; }
-    set_error("tt_local_search: not implemented yet");
-    return TT_ERR_LIMIT;
+    int rc = check_pop_args(p, P, slot, room);
+    if (rc || P == 0) return rc;
+    if (!rng) { set_error("null rng buffer"); return TT_ERR_INVALID; }
+    if (max_steps < 0) { set_error("negative max_steps"); return TT_ERR_INVALID; }
+    if ((rc = use_device(p))) return rc;
+    const LsLayout L = ls_layout(p->E, p->R, p->dev.EW64);
+    if (L.bytes > 160 * 1024) { set_error("instance too large for the local-search kernel"); return TT_ERR_LIMIT; }
+    hipLaunchKernelGGL(local_search_kernel, dim3(P), dim3(64), L.bytes, (hipStream_t)stream, p->dev, slot, room, rng,
+                       P, max_steps, p1, p2, p3);
+    return check_hip(hipGetLastError(), "local_search launch");
 }

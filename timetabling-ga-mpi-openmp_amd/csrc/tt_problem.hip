@@ -104,6 +104,10 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
             const int j = cp_j[k];
             cupT[(size_t)(j >> 6) * E + i] |= 1ull << (j & 63);
         }
+    std::vector<uint64_t> corr64((size_t)E * EW64, 0ull);
+    for (int i = 0; i < E; i++)
+        for (int j = 0; j < E; j++)
+            if (p->corr_bits[(size_t)i * EW + (j >> 5)] >> (j & 31) & 1u) corr64[(size_t)i * EW64 + (j >> 6)] |= 1ull << (j & 63);
     std::vector<int32_t> stc_off(S + 1, 0), stc_ev;
     for (int s = 0; s < S; s++) {
         for (int k = stu_off[s]; k < stu_off[s + 1]; k++) stc_ev.push_back(stu_ev[k]);
@@ -140,6 +144,7 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         {cupT.data(), sizeof(uint64_t) * cupT.size(), 0},
         {stc_off.data(), sizeof(int32_t) * stc_off.size(), 0},
         {stc_ev.data(), sizeof(int32_t) * stc_ev.size(), 0},
+        {corr64.data(), sizeof(uint64_t) * corr64.size(), 0},
     };
     size_t total = 0;
     for (auto& q : parts) { q.off = total; total += (q.bytes + 255) & ~(size_t)255; }
@@ -175,6 +180,7 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     d.cupT = (const uint64_t*)(base + parts[10].off);
     d.stc_off = (const int32_t*)(base + parts[11].off);
     d.stc_ev = (const int32_t*)(base + parts[12].off);
+    d.corr64 = (const uint64_t*)(base + parts[13].off);
     *out = p;
     return TT_OK;
 }
