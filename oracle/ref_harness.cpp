@@ -187,6 +187,28 @@ void ref_local_search(void* p, u8* slot, u8* room, long* rng, int np, int max_st
     }
 }
 
+// localSearch over a population, OpenMP over individuals (each with its own
+// Random, so the result equals the serial ref_local_search). Returns seconds.
+double ref_local_search_timed(void* p, u8* slot, u8* room, long* rng, int np, int max_steps, int threads) {
+    Problem* P = (Problem*)p;
+    const int E = P->n_of_events;
+    omp_set_num_threads(threads);
+    struct timeval t0, t1;
+    gettimeofday(&t0, 0);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int i = 0; i < np; i++) {
+        Random r(0);
+        r.seed = rng[i];
+        Solution s(P, &r);
+        load_solution(&s, slot + (long)i * E, room + (long)i * E, E);
+        s.localSearch(max_steps);
+        store_solution(&s, slot + (long)i * E, room + (long)i * E, E);
+        rng[i] = r.seed;
+    }
+    gettimeofday(&t1, 0);
+    return (t1.tv_sec - t0.tv_sec) + 1e-6 * (t1.tv_usec - t0.tv_usec);
+}
+
 // Crossover into a FRESH child (no prior RandomInitialSolution), i.e. the
 // reference's crossover without the F2 stale-list defect.
 void ref_crossover(void* p, const u8* slot1, const u8* slot2, long* rng, u8* slot, u8* room, int np) {

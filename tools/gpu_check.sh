@@ -26,6 +26,8 @@ for s in $STEPS; do
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py ;;
     phases) run phases 300 python -u tools/prof_eval.py med 65536 ;;
+    ls)    run bench_ls 600 python -u tools/bench_ls.py --pop 4096 --steps 200 ;;
+    ls1000) run bench_ls1000 600 python -u tools/bench_ls.py --pop 4096 --steps 1000 --cpu-sample 256 ;;
     listpmc) run listpmc 120 rocprofv3 -L ;;
     pmc1)  run pmc1 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS --output-format csv -d "$OUT/pmc1" -o pmc -- python -u bench.py --no-cpu --steps 3 --warmup 1 ;;
     pmc2)  run pmc2 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc2" -o pmc -- python -u bench.py --no-cpu --steps 3 --warmup 1 ;;
