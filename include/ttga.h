@@ -26,6 +26,7 @@
 #ifndef TTGA_H
 #define TTGA_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -99,6 +100,35 @@ int tt_mutation(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng,
  * bound (999999 s by default, never binding) is not modelled. */
 int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P, int max_steps,
                     double p1, double p2, double p3, void* stream);
+
+/* ---- GA generation primitives (ga.cpp:510-588, batched over C children) ----
+ * Population (caller-owned, device): pop_slot/pop_room [N][E], pop_hcv,
+ * pop_scv, pop_penalty i32[N], pop_feasible u8[N]; kept sorted by penalty.
+ *
+ * tt_ga_breed: for every child c, on its own stream rng[c], in the reference's
+ * per-generation draw order (ga.cpp:543-571): optionally the 3*E draws of the
+ * three discarded RandomInitialSolution calls (ga.cpp:543-548), two
+ * selection5 tournaments over pop_penalty (ga.cpp:129-145), next() < p_cross ?
+ * crossover of the two parents : copy of the first (ga.cpp:562-566), then
+ * next() < p_mut ? randomMove (ga.cpp:569-571). Children come out with rooms
+ * assigned, ready for tt_local_search + tt_eval. child_flags u8[C] (scratch:
+ * bit 0 crossed, bit 1 mutated). */
+int tt_ga_breed(const tt_problem* p, const uint8_t* pop_slot, const uint8_t* pop_room, const int32_t* pop_penalty,
+                int N, int64_t* rng, int C, double p_cross, double p_mut, int skip_init_draws, uint8_t* child_slot,
+                uint8_t* child_room, uint8_t* child_flags, void* stream);
+
+/* Bytes of device scratch tt_ga_replace needs for a population of N. */
+size_t tt_ga_work_bytes(int N, int E);
+
+/* tt_ga_replace: the C evaluated children overwrite population positions
+ * N-C..N-1 (ga.cpp:582, "pop[popSize-1]->copy(child)" for C = 1), then the
+ * population is sorted by penalty ascending (ga.cpp:583; ties keep position
+ * order, std::sort leaves them unspecified). In place; `work` has
+ * tt_ga_work_bytes(N, E) bytes. */
+int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* pop_room, int32_t* pop_hcv, int32_t* pop_scv,
+                  uint8_t* pop_feasible, int32_t* pop_penalty, int N, const uint8_t* child_slot,
+                  const uint8_t* child_room, const int32_t* child_hcv, const int32_t* child_scv,
+                  const uint8_t* child_feasible, const int32_t* child_penalty, int C, void* work, void* stream);
 
 /* Device-side status word of the problem handle (0 = fine; bit 0 = a slot
  * exceeded 256 events in a matching). Synchronises the device. */

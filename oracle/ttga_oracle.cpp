@@ -725,6 +725,77 @@ void tto_mutation(const void* p, uint8_t* slot, uint8_t* room, int64_t* rng, int
     }
 }
 
+// GA generation primitives (the batched restatement of ga.cpp:543-585, see
+// include/ttga.h tt_ga_breed / tt_ga_replace). Child c uses stream rng[c].
+void tto_ga_breed(const void* p, const uint8_t* pop_slot, const uint8_t* pop_room, const int32_t* pen, int N,
+                  int64_t* rng, int C, double p_cross, double p_mut, int skip_init, uint8_t* child_slot,
+                  uint8_t* child_room, uint8_t* flags) {
+    const Problem& P = *(const Problem*)p;
+    const int E = P.E;
+    Sol s;
+    for (int c = 0; c < C; c++) {
+        long st = (long)rng[c];
+        if (skip_init)                                        // ga.cpp:543-548
+            for (int k = 0; k < 3 * E; k++) pm_next(&st);
+        int par[2];
+        for (int q = 0; q < 2; q++) {                         // selection5, ga.cpp:129-145
+            int best = (int)(pm_next(&st) * N);
+            for (int i = 1; i < 5; i++) {
+                int t = (int)(pm_next(&st) * N);
+                if (pen[t] < pen[best]) best = t;
+            }
+            par[q] = best;
+        }
+        uint8_t f = 0;
+        const uint8_t* sa = pop_slot + (size_t)par[0] * E;
+        const uint8_t* sb = pop_slot + (size_t)par[1] * E;
+        if (pm_next(&st) < p_cross) {                         // ga.cpp:562-563
+            f |= 1;
+            s.slot.assign(E, 0);
+            s.room.assign(E, -1);
+            for (int e = 0; e < E; e++) s.slot[e] = pm_next(&st) < 0.5 ? sa[e] : sb[e];
+            build_lists(s);
+            assign_all(P, s);
+        } else {                                              // ga.cpp:564-566
+            load(P, s, sa, pop_room + (size_t)par[0] * E);
+        }
+        if (pm_next(&st) < p_mut) {                           // ga.cpp:569-571
+            f |= 2;
+            random_move(P, s, &st);
+        }
+        store(P, s, child_slot + (size_t)c * E, child_room + (size_t)c * E);
+        flags[c] = f;
+        rng[c] = st;
+    }
+}
+
+// children overwrite positions N-C..N-1 (ga.cpp:582), then a stable sort by
+// penalty (ga.cpp:583).
+void tto_ga_replace(const void* p, uint8_t* pop_slot, uint8_t* pop_room, int32_t* hcv, int32_t* scv, uint8_t* feas,
+                    int32_t* pen, int N, const uint8_t* cs, const uint8_t* cr, const int32_t* ch, const int32_t* csc,
+                    const uint8_t* cf, const int32_t* cp, int C) {
+    const Problem& P = *(const Problem*)p;
+    const int E = P.E, k = N - C;
+    for (int c = 0; c < C; c++) {
+        memcpy(pop_slot + (size_t)(k + c) * E, cs + (size_t)c * E, E);
+        memcpy(pop_room + (size_t)(k + c) * E, cr + (size_t)c * E, E);
+        hcv[k + c] = ch[c]; scv[k + c] = csc[c]; feas[k + c] = cf[c]; pen[k + c] = cp[c];
+    }
+    std::vector<int> idx(N);
+    for (int i = 0; i < N; i++) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return pen[a] < pen[b]; });
+    std::vector<uint8_t> s2((size_t)N * E), r2((size_t)N * E), f2(N);
+    std::vector<int32_t> h2(N), sc2(N), p2(N);
+    for (int i = 0; i < N; i++) {
+        memcpy(&s2[(size_t)i * E], pop_slot + (size_t)idx[i] * E, E);
+        memcpy(&r2[(size_t)i * E], pop_room + (size_t)idx[i] * E, E);
+        h2[i] = hcv[idx[i]]; sc2[i] = scv[idx[i]]; f2[i] = feas[idx[i]]; p2[i] = pen[idx[i]];
+    }
+    memcpy(pop_slot, s2.data(), s2.size());
+    memcpy(pop_room, r2.data(), r2.size());
+    for (int i = 0; i < N; i++) { hcv[i] = h2[i]; scv[i] = sc2[i]; feas[i] = f2[i]; pen[i] = p2[i]; }
+}
+
 // Single move primitives for unit tests (Move1/2/3, Solution.cpp:357-439).
 void tto_move(const void* p, uint8_t* slot, uint8_t* room, int type, int a, int b, int c) {
     const Problem& P = *(const Problem*)p;

@@ -44,6 +44,9 @@ class _Checker:
         getattr(L, pre + "local_search").argtypes = [_vp, _vp, _vp, _vp, i32, i32, dbl, dbl, dbl]
         getattr(L, pre + "crossover").argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, i32]
         getattr(L, pre + "mutation").argtypes = [_vp, _vp, _vp, _vp, i32]
+        if hasattr(L, pre + "ga_breed"):
+            getattr(L, pre + "ga_breed").argtypes = [_vp, _vp, _vp, _vp, i32, _vp, i32, dbl, dbl, i32, _vp, _vp, _vp]
+            getattr(L, pre + "ga_replace").argtypes = [_vp] + [_vp] * 6 + [i32] + [_vp] * 6 + [i32]
 
     def _f(self, name):
         return getattr(self.lib, self.prefix + name)
@@ -122,6 +125,31 @@ class _Handle:
         rng = np.ascontiguousarray(seeds, np.int64).copy()
         self.c._f("mutation")(self.h, _p(slot), _p(room), _p(rng), slot.shape[0])
         return slot, room, rng
+
+
+def _ga_breed(self, pop_slot, pop_room, pen, seeds, C, p_cross=0.8, p_mut=0.5, skip_init=1):
+    pop_slot = np.ascontiguousarray(pop_slot, np.uint8); pop_room = np.ascontiguousarray(pop_room, np.uint8)
+    pen = np.ascontiguousarray(pen, np.int32)
+    rng = np.ascontiguousarray(seeds, np.int64).copy()
+    cs = np.zeros((C, self.E), np.uint8); cr = np.zeros((C, self.E), np.uint8); fl = np.zeros(C, np.uint8)
+    self.c._f("ga_breed")(self.h, _p(pop_slot), _p(pop_room), _p(pen), pop_slot.shape[0], _p(rng), C,
+                          float(p_cross), float(p_mut), int(skip_init), _p(cs), _p(cr), _p(fl))
+    return cs, cr, fl, rng
+
+
+def _ga_replace(self, pop, child):
+    """pop/child: dicts with slot, room, hcv, scv, feasible, penalty (numpy); returns the new pop."""
+    out = {k: np.ascontiguousarray(v).copy() for k, v in pop.items()}
+    ch = {k: np.ascontiguousarray(v) for k, v in child.items()}
+    N, C = out["slot"].shape[0], ch["slot"].shape[0]
+    self.c._f("ga_replace")(self.h, _p(out["slot"]), _p(out["room"]), _p(out["hcv"]), _p(out["scv"]),
+                            _p(out["feasible"]), _p(out["penalty"]), N, _p(ch["slot"]), _p(ch["room"]),
+                            _p(ch["hcv"]), _p(ch["scv"]), _p(ch["feasible"]), _p(ch["penalty"]), C)
+    return out
+
+
+_Handle.ga_breed = _ga_breed
+_Handle.ga_replace = _ga_replace
 
 
 class Oracle(_Checker):

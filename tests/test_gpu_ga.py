@@ -1,0 +1,126 @@
+"""GA engine on the GPU vs the CPU restatement: breeding (selection5,
+crossover/copy, mutation), replace-worst + sort, whole island generations, and
+the ga.cpp-style driver end to end. Bit-exact."""
+import json
+import pathlib
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import ttga
+from oracle_lib import oracle
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+from ttga import native  # noqa: E402
+from ttga.ga import Island, stream_seeds  # noqa: E402
+
+REPO = pathlib.Path(__file__).resolve().parent.parent
+KEYS = ("slot", "room", "hcv", "scv", "feasible", "penalty")
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def oracle_population(o, N, seed, steps):
+    s, r, g = o.random_init(stream_seeds(seed, 0, N))
+    s, r, g = o.local_search(s, r, g, steps)
+    h, sc, f, p = o.eval(s, r)
+    pop = dict(slot=s, room=r, hcv=h, scv=sc, feasible=f, penalty=p)
+    empty = {k: v[:0] for k, v in pop.items()}
+    return o.ga_replace(pop, empty)
+
+
+@pytest.fixture(scope="module")
+def sm():
+    inst = ttga.config_instance("sm")
+    return inst, native.DeviceProblem(inst), oracle().problem(inst)
+
+
+@pytest.mark.parametrize("N,C,skip", [(10, 1, 1), (10, 10, 1), (64, 37, 0), (200, 130, 1)])
+def test_breed_vs_oracle(sm, N, C, skip):
+    inst, dp, o = sm
+    pop = oracle_population(o, N, 3 + N, 50)
+    seeds = stream_seeds(11 + C, N, C)
+    cs, cr, fl, rng = o.ga_breed(pop["slot"], pop["room"], pop["penalty"], seeds, C, 0.8, 0.5, skip)
+    gs, gr = dev(np.zeros((C, inst.E), np.uint8)), dev(np.zeros((C, inst.E), np.uint8))
+    gf, grng = dev(np.zeros(C, np.uint8)), dev(seeds)
+    dp.ga_breed(dev(pop["slot"]), dev(pop["room"]), dev(pop["penalty"]), grng, gs, gr, gf, 0.8, 0.5, bool(skip))
+    assert np.array_equal(host(gf), fl)
+    assert np.array_equal(host(gs), cs) and np.array_equal(host(gr), cr)
+    assert np.array_equal(host(grng), rng)
+    assert (fl & 1).any() and (fl & 2).any() if C >= 10 else True
+
+
+@pytest.mark.parametrize("N,C", [(10, 1), (10, 4), (300, 300), (5000, 100)])
+def test_replace_vs_oracle(sm, N, C):
+    inst, dp, o = sm
+    rng = np.random.default_rng(N + C)
+    def rand_pop(n):
+        pen = rng.integers(0, 40, n).astype(np.int32)       # many ties: checks the stable order
+        return dict(slot=rng.integers(0, 45, (n, inst.E), dtype=np.uint8),
+                    room=rng.integers(0, inst.R, (n, inst.E), dtype=np.uint8),
+                    hcv=rng.integers(0, 9, n).astype(np.int32), scv=rng.integers(0, 99, n).astype(np.int32),
+                    feasible=rng.integers(0, 2, n).astype(np.uint8), penalty=pen)
+    pop, ch = rand_pop(N), rand_pop(C)
+    exp = o.ga_replace(pop, ch)
+    gpop = {k: dev(v) for k, v in pop.items()}
+    dp.ga_replace(gpop, {k: dev(v) for k, v in ch.items()}, dp.ga_work(N))
+    for k in KEYS:
+        assert np.array_equal(host(gpop[k]), exp[k]), k
+
+
+@pytest.mark.parametrize("N,C,gens", [(10, 1, 12), (16, 8, 6)])
+def test_island_generations_vs_oracle(sm, N, C, gens):
+    inst, dp, o = sm
+    steps, seed = 120, 29
+    isl = Island(dp, pop_size=N, children=C, max_steps=steps, seed=seed)
+    isl.initialize()
+    for _ in range(gens):
+        isl.step()
+    pop = oracle_population(o, N, seed, steps)
+    rng = stream_seeds(seed, N, C)
+    for _ in range(gens):
+        cs, cr, fl, rng = o.ga_breed(pop["slot"], pop["room"], pop["penalty"], rng, C, 0.8, 0.5, 1)
+        cs, cr, rng = o.local_search(cs, cr, rng, steps)
+        h, sc, f, p = o.eval(cs, cr)
+        pop = o.ga_replace(pop, dict(slot=cs, room=cr, hcv=h, scv=sc, feasible=f, penalty=p))
+    for k in KEYS:
+        assert np.array_equal(host(isl.pop[k]), pop[k]), k
+    assert np.array_equal(host(isl.rng_child), rng)
+    assert np.all(np.diff(pop["penalty"]) >= 0)
+
+
+def test_islands_cli_end_to_end(tmp_path, sm):
+    """python -m ttga.islands on one GPU: Control-style CLI, JSON lines in the
+    reference's format, one self-migration (generation 49), and the printed
+    timetable re-evaluates to the printed totalBest."""
+    inst, dp, o = sm
+    tim = tmp_path / "sm.tim"
+    ttga.write_tim(inst, tim)
+    cmd = [sys.executable, "-m", "ttga.islands", "-i", str(tim), "-s", "42", "-p", "1", "-c", "2",
+           "--generations", "60"]
+    env = dict(__import__("os").environ, PYTHONPATH=str(REPO / "timetabling-ga-mpi-openmp_amd"))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    objs = [json.loads(ln) for ln in lines]
+    assert "Max number of threads 2" in r.stdout
+    assert any("logEntry" in x for x in objs)
+    runs = [x["runEntry"] for x in objs if "runEntry" in x]
+    assert runs[0].keys() == {"feasible", "totalBest"} and runs[-1]["procsNum"] == 1 and runs[-1]["threadsNum"] == 2
+    sol = [x["solution"] for x in objs if "solution" in x][0]
+    assert sol["procID"] == 0 and sol["threadID"] == 0
+    if sol["feasible"]:
+        s = np.array(sol["timeslots"], np.uint8)[None]
+        rm = np.array(sol["rooms"], np.uint8)[None]
+        h, sc, f, p = o.eval(s, rm)
+        assert f[0] == 1 and sc[0] == sol["totalBest"] == runs[0]["totalBest"]

@@ -1,0 +1,271 @@
+// GA generation primitives, batched over the children of one generation
+// (ga.cpp:543-585 per child; C children are bred from the same population
+// snapshot, the batched counterpart of the reference's OpenMP threads):
+//
+//   tt_ga_breed    per child c, on its own stream rng[c] (A.6 order):
+//                    [3*E draws of the three discarded RandomInitialSolution, ga.cpp:543-548]
+//                    parent a = selection5(pop), parent b = selection5(pop)   (ga.cpp:129-145,551-552)
+//                    next() < p_cross ? crossover(a, b) : copy of a         (ga.cpp:562-566)
+//                    next() < p_mut   ? randomMove                           (ga.cpp:569-571)
+//   tt_ga_replace  children overwrite positions N-C..N-1 (ga.cpp:582 with
+//                  C = 1), then the population is sorted by penalty
+//                  ascending (ga.cpp:583); ties keep position order.
+#include <algorithm>
+
+#include "tt_internal.h"
+#include "tt_match.h"
+
+namespace ttga {
+
+constexpr uint8_t kFlagCross = 1, kFlagMutate = 2;
+
+// ---------------------------------------------------------------- breed
+// Lane per child for the RNG-sequential part (selection, the E crossover
+// draws recorded as a bitmask in LDS, the mutation draw); then the wave builds
+// each child row with coalesced reads of its parents' rows.
+__global__ __launch_bounds__(64) void breed_kernel(int E, const uint8_t* __restrict__ pop_slot,
+                                                   const uint8_t* __restrict__ pop_room,
+                                                   const int32_t* __restrict__ pen, int N,
+                                                   int64_t* __restrict__ rng, int C, double p_cross, double p_mut,
+                                                   int skip_init, uint8_t* __restrict__ child_slot,
+                                                   uint8_t* __restrict__ child_room, uint8_t* __restrict__ flags) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x;
+    const int EW = (E + 63) / 64;
+    uint64_t* pick = (uint64_t*)lds;                 // [64][EW] bit e set: take parent a's slot
+    int32_t* par = (int32_t*)(pick + 64 * EW);       // [64][2]
+    uint8_t* fl = (uint8_t*)(par + 128);             // [64]
+    const long c0 = (long)blockIdx.x * 64;
+    const int nc = (int)min((long)64, (long)C - c0);
+    if (lane < nc) {
+        int64_t s = rng[c0 + lane];
+        if (skip_init)
+            for (int k = 0; k < 3 * E; ++k) pm_next(s);
+        int best[2];
+        for (int q = 0; q < 2; ++q) {                 // selection5 (ga.cpp:129-145)
+            int b = pm_pick(s, N);
+            for (int i = 1; i < 5; ++i) {
+                const int t = pm_pick(s, N);
+                if (pen[t] < pen[b]) b = t;
+            }
+            best[q] = b;
+        }
+        uint8_t f = 0;
+        uint64_t* pk = pick + lane * EW;
+        if (pm_next(s) < p_cross) {                   // crossover (Solution.cpp:896-903)
+            f |= kFlagCross;
+            for (int w = 0; w < EW; ++w) {
+                uint64_t m = 0;
+                const int n = min(64, E - 64 * w);
+                for (int b = 0; b < n; ++b)
+                    if (pm_next(s) < 0.5) m |= 1ull << b;
+                pk[w] = m;
+            }
+        }
+        if (pm_next(s) < p_mut) f |= kFlagMutate;
+        rng[c0 + lane] = s;
+        par[2 * lane] = best[0];
+        par[2 * lane + 1] = best[1];
+        fl[lane] = f;
+    }
+    __syncthreads();
+    for (int c = 0; c < nc; ++c) {
+        const long ch = c0 + c;
+        const int a = par[2 * c], b = par[2 * c + 1];
+        const uint8_t f = fl[c];
+        const uint8_t* sa = pop_slot + (long)a * E;
+        const uint8_t* sb = pop_slot + (long)b * E;
+        const uint8_t* ra = pop_room + (long)a * E;
+        const uint64_t* pk = pick + c * EW;
+        for (int e = lane; e < E; e += 64) {
+            if (f & kFlagCross) {
+                child_slot[ch * E + e] = ((pk[e >> 6] >> (e & 63)) & 1ull) ? sa[e] : sb[e];
+            } else {
+                child_slot[ch * E + e] = sa[e];
+                child_room[ch * E + e] = ra[e];
+            }
+        }
+        if (lane == 0) flags[ch] = f;
+    }
+}
+
+// ---------------------------------------------------------------- replace + sort
+__device__ __forceinline__ uint64_t sort_key(int32_t penalty, int pos) {
+    return ((uint64_t)((uint32_t)penalty ^ 0x80000000u) << 32) | (uint32_t)pos;
+}
+
+// keys of the merged population: positions < N-C from pop, the rest from the children
+__global__ void replace_keys_kernel(const int32_t* __restrict__ pen, const int32_t* __restrict__ cpen, int N, int C,
+                                    int NP, uint64_t* __restrict__ keys) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= NP) return;
+    if (i >= N) { keys[i] = ~0ull; return; }
+    const int k = N - C;
+    keys[i] = sort_key(i < k ? pen[i] : cpen[i - k], i);
+}
+
+// bitonic sort of NP (power of two) u64 keys: one workgroup in LDS when NP <= 4096 ...
+__global__ __launch_bounds__(1024) void bitonic_lds_kernel(uint64_t* __restrict__ keys, int NP) {
+    __shared__ uint64_t sk[4096];
+    for (int i = threadIdx.x; i < NP; i += blockDim.x) sk[i] = keys[i];
+    __syncthreads();
+    for (int k = 2; k <= NP; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < NP; i += blockDim.x) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const uint64_t x = sk[i], y = sk[l];
+                    const bool up = (i & k) == 0;
+                    if ((x > y) == up) { sk[i] = y; sk[l] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < NP; i += blockDim.x) keys[i] = sk[i];
+}
+
+// ... one global pass per (k, j) stage above that
+__global__ void bitonic_step_kernel(uint64_t* __restrict__ keys, int NP, int k, int j) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= NP) return;
+    const int l = i ^ j;
+    if (l > i) {
+        const uint64_t x = keys[i], y = keys[l];
+        const bool up = (i & k) == 0;
+        if ((x > y) == up) { keys[i] = y; keys[l] = x; }
+    }
+}
+
+// gather the sorted population into the work rows (one wave per row)
+__global__ __launch_bounds__(64) void replace_gather_kernel(int E, int N, int C, const uint64_t* __restrict__ keys,
+                                                            const uint8_t* __restrict__ ps, const uint8_t* __restrict__ pr,
+                                                            const int32_t* __restrict__ ph, const int32_t* __restrict__ psc,
+                                                            const uint8_t* __restrict__ pf, const int32_t* __restrict__ pp,
+                                                            const uint8_t* __restrict__ cs, const uint8_t* __restrict__ cr,
+                                                            const int32_t* __restrict__ ch, const int32_t* __restrict__ csc,
+                                                            const uint8_t* __restrict__ cf, const int32_t* __restrict__ cp,
+                                                            uint8_t* __restrict__ ws, uint8_t* __restrict__ wr,
+                                                            int32_t* __restrict__ wm) {
+    const int i = blockIdx.x;
+    const int src = (int)(keys[i] & 0xFFFFFFFFu);
+    const int k = N - C;
+    const bool child = src >= k;
+    const int r = child ? src - k : src;
+    const uint8_t* s = (child ? cs : ps) + (long)r * E;
+    const uint8_t* m = (child ? cr : pr) + (long)r * E;
+    for (int e = threadIdx.x; e < E; e += 64) {
+        ws[(long)i * E + e] = s[e];
+        wr[(long)i * E + e] = m[e];
+    }
+    if (threadIdx.x == 0) {
+        wm[4 * i + 0] = child ? ch[r] : ph[r];
+        wm[4 * i + 1] = child ? csc[r] : psc[r];
+        wm[4 * i + 2] = child ? cf[r] : pf[r];
+        wm[4 * i + 3] = child ? cp[r] : pp[r];
+    }
+}
+
+__global__ __launch_bounds__(64) void replace_scatter_kernel(int E, const uint8_t* __restrict__ ws,
+                                                             const uint8_t* __restrict__ wr,
+                                                             const int32_t* __restrict__ wm, uint8_t* __restrict__ ps,
+                                                             uint8_t* __restrict__ pr, int32_t* __restrict__ ph,
+                                                             int32_t* __restrict__ psc, uint8_t* __restrict__ pf,
+                                                             int32_t* __restrict__ pp) {
+    const int i = blockIdx.x;
+    for (int e = threadIdx.x; e < E; e += 64) {
+        ps[(long)i * E + e] = ws[(long)i * E + e];
+        pr[(long)i * E + e] = wr[(long)i * E + e];
+    }
+    if (threadIdx.x == 0) {
+        ph[i] = wm[4 * i + 0];
+        psc[i] = wm[4 * i + 1];
+        pf[i] = (uint8_t)wm[4 * i + 2];
+        pp[i] = wm[4 * i + 3];
+    }
+}
+
+static int pow2_at_least(int n) {
+    int p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+}  // namespace ttga
+
+using namespace ttga;
+
+// launched from tt_rooms.hip (masked variants of the matcher and of mutation)
+namespace ttga {
+int launch_assign_masked(const tt_problem* p, const uint8_t* slot, uint8_t* room, int P, const uint8_t* mask,
+                         uint8_t bit, hipStream_t st);
+int launch_mutation_masked(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P,
+                           const uint8_t* mask, uint8_t bit, hipStream_t st);
+}  // namespace ttga
+
+extern "C" int tt_ga_breed(const tt_problem* p, const uint8_t* pop_slot, const uint8_t* pop_room,
+                           const int32_t* pop_penalty, int N, int64_t* rng, int C, double p_cross, double p_mut,
+                           int skip_init_draws, uint8_t* child_slot, uint8_t* child_room, uint8_t* child_flags,
+                           void* stream) {
+    int rc = check_pop_args(p, C, child_slot, child_room);
+    if (rc) return rc;
+    if (N < 1 || !pop_slot || !pop_room || !pop_penalty || (C > 0 && (!rng || !child_flags))) {
+        set_error("tt_ga_breed: bad population arguments");
+        return TT_ERR_INVALID;
+    }
+    if (C == 0) return TT_OK;
+    if ((rc = use_device(p))) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const int EW = (p->E + 63) / 64;
+    const size_t lds = 8 * (size_t)64 * EW + 4 * 128 + 64;
+    hipLaunchKernelGGL(breed_kernel, dim3((C + 63) / 64), dim3(64), lds, st, p->E, pop_slot, pop_room, pop_penalty, N,
+                       rng, C, p_cross, p_mut, skip_init_draws, child_slot, child_room, child_flags);
+    if ((rc = check_hip(hipGetLastError(), "breed launch"))) return rc;
+    if ((rc = launch_assign_masked(p, child_slot, child_room, C, child_flags, kFlagCross, st))) return rc;
+    return launch_mutation_masked(p, child_slot, child_room, rng, C, child_flags, kFlagMutate, st);
+}
+
+extern "C" size_t tt_ga_work_bytes(int N, int E) {
+    if (N < 1 || E < 1) return 0;
+    const size_t NP = (size_t)pow2_at_least(N);
+    return align256(8 * NP) + 2 * align256((size_t)N * E) + align256(16 * (size_t)N);
+}
+
+extern "C" int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* pop_room, int32_t* pop_hcv,
+                             int32_t* pop_scv, uint8_t* pop_feasible, int32_t* pop_penalty, int N,
+                             const uint8_t* child_slot, const uint8_t* child_room, const int32_t* child_hcv,
+                             const int32_t* child_scv, const uint8_t* child_feasible, const int32_t* child_penalty,
+                             int C, void* work, void* stream) {
+    if (!p || N < 1 || C < 0 || C > N || !work || !pop_slot || !pop_room || !pop_hcv || !pop_scv || !pop_feasible ||
+        !pop_penalty || (C > 0 && (!child_slot || !child_room || !child_hcv || !child_scv || !child_feasible ||
+                                   !child_penalty))) {
+        set_error("tt_ga_replace: bad arguments");
+        return TT_ERR_INVALID;
+    }
+    int rc = use_device(p);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const int E = p->E, NP = pow2_at_least(N);
+    uint8_t* w = (uint8_t*)work;
+    uint64_t* keys = (uint64_t*)w;
+    uint8_t* ws = w + align256(8 * (size_t)NP);
+    uint8_t* wr = ws + align256((size_t)N * E);
+    int32_t* wm = (int32_t*)(wr + align256((size_t)N * E));
+    hipLaunchKernelGGL(replace_keys_kernel, dim3((NP + 255) / 256), dim3(256), 0, st, pop_penalty, child_penalty, N, C,
+                       NP, keys);
+    if (NP <= 4096) {
+        hipLaunchKernelGGL(bitonic_lds_kernel, dim3(1), dim3(std::min(NP, 1024)), 0, st, keys, NP);
+    } else {
+        for (int k = 2; k <= NP; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1)
+                hipLaunchKernelGGL(bitonic_step_kernel, dim3((NP + 255) / 256), dim3(256), 0, st, keys, NP, k, j);
+    }
+    hipLaunchKernelGGL(replace_gather_kernel, dim3(N), dim3(64), 0, st, E, N, C, keys, pop_slot, pop_room, pop_hcv,
+                       pop_scv, pop_feasible, pop_penalty, child_slot, child_room, child_hcv, child_scv, child_feasible,
+                       child_penalty, ws, wr, wm);
+    hipLaunchKernelGGL(replace_scatter_kernel, dim3(N), dim3(64), 0, st, E, ws, wr, wm, pop_slot, pop_room, pop_hcv,
+                       pop_scv, pop_feasible, pop_penalty);
+    return check_hip(hipGetLastError(), "tt_ga_replace launch");
+}

@@ -21,10 +21,12 @@ __device__ inline void store_row(uint8_t* dst, const uint8_t* src, int E, int la
 
 // ---------------------------------------------------------------- assign
 __global__ __launch_bounds__(64) void assign_rooms_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
-                                                          uint8_t* __restrict__ room, int P) {
+                                                          uint8_t* __restrict__ room, int P,
+                                                          const uint8_t* __restrict__ mask, uint8_t bit) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int E = pb.E, lane = threadIdx.x;
     const long p = blockIdx.x;
+    if (mask && !(mask[p] & bit)) return;
     MatchScratch m = carve_match_scratch(lds, E, pb.R);
     load_row(m.sl, slot + p * E, E, lane);
     for (int e = lane; e < E; e += 64) m.rr[e] = 0xFF;   // events with an invalid slot stay 255
@@ -101,10 +103,11 @@ __global__ __launch_bounds__(64) void crossover_slots_kernel(int E, const uint8_
 // touched twice gets the same rooms both times).
 __global__ __launch_bounds__(64) void mutation_kernel(DevProblem pb, uint8_t* __restrict__ slot,
                                                       uint8_t* __restrict__ room, int64_t* __restrict__ rng,
-                                                      int P) {
+                                                      int P, const uint8_t* __restrict__ mask, uint8_t bit) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int E = pb.E, lane = threadIdx.x;
     const long p = blockIdx.x;
+    if (mask && !(mask[p] & bit)) return;
     MatchScratch m = carve_match_scratch(lds, E, pb.R);
     load_row(m.sl, slot + p * E, E, lane);
     load_row(m.rr, room + p * E, E, lane);
@@ -151,11 +154,24 @@ __global__ __launch_bounds__(64) void mutation_kernel(DevProblem pb, uint8_t* __
 
 static int tile_stride(int E) { return (E + 3) & ~3; }
 
-static int launch_assign(const tt_problem* p, const uint8_t* slot, uint8_t* room, int P, hipStream_t st) {
+int launch_assign_masked(const tt_problem* p, const uint8_t* slot, uint8_t* room, int P, const uint8_t* mask,
+                         uint8_t bit, hipStream_t st) {
     const size_t lds = match_scratch_bytes(p->E, p->R);
     if (lds > 160 * 1024) { set_error("instance too large for the matcher"); return TT_ERR_LIMIT; }
-    hipLaunchKernelGGL(assign_rooms_kernel, dim3(P), dim3(64), lds, st, p->dev, slot, room, P);
+    hipLaunchKernelGGL(assign_rooms_kernel, dim3(P), dim3(64), lds, st, p->dev, slot, room, P, mask, bit);
     return check_hip(hipGetLastError(), "assign_rooms launch");
+}
+
+int launch_mutation_masked(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P,
+                           const uint8_t* mask, uint8_t bit, hipStream_t st) {
+    const size_t lds = match_scratch_bytes(p->E, p->R);
+    if (lds > 160 * 1024) { set_error("instance too large for the matcher"); return TT_ERR_LIMIT; }
+    hipLaunchKernelGGL(mutation_kernel, dim3(P), dim3(64), lds, st, p->dev, slot, room, rng, P, mask, bit);
+    return check_hip(hipGetLastError(), "mutation launch");
+}
+
+static int launch_assign(const tt_problem* p, const uint8_t* slot, uint8_t* room, int P, hipStream_t st) {
+    return launch_assign_masked(p, slot, room, P, nullptr, 0, st);
 }
 
 }  // namespace ttga
@@ -202,8 +218,5 @@ extern "C" int tt_mutation(const tt_problem* p, uint8_t* slot, uint8_t* room, in
     if (rc || P == 0) return rc;
     if (!rng) { set_error("null rng buffer"); return TT_ERR_INVALID; }
     if ((rc = use_device(p))) return rc;
-    const size_t lds = match_scratch_bytes(p->E, p->R);
-    if (lds > 160 * 1024) { set_error("instance too large for the matcher"); return TT_ERR_LIMIT; }
-    hipLaunchKernelGGL(mutation_kernel, dim3(P), dim3(64), lds, (hipStream_t)stream, p->dev, slot, room, rng, P);
-    return check_hip(hipGetLastError(), "mutation launch");
+    return launch_mutation_masked(p, slot, room, rng, P, nullptr, 0, (hipStream_t)stream);
 }

@@ -1,0 +1,181 @@
+"""The GA of ga.cpp on the device: one island per GPU, batched generations.
+
+Mirrors ga.cpp:370-613 with the per-child operators running as batched
+kernels (include/ttga.h):
+
+* initial population: RandomInitialSolution + localSearch(maxSteps) +
+  computePenalty per member (ga.cpp:429-434), then sorted;
+* a generation breeds C children from the current population
+  (tt_ga_breed: selection5 x2, crossover p=0.8 / copy, mutation p=0.5),
+  runs localSearch + evaluation on all of them, and replaces the C worst
+  members, re-sorting by penalty (tt_ga_replace). C = 1 is the reference's
+  single-thread steady state; C > 1 is the batched counterpart of its
+  OpenMP threads (every thread breeding against the shared population);
+* migration (ga.cpp:514-540) and the final MIN reduction (ga.cpp:234-257) are
+  in ttga.islands.
+
+Each population member and each child slot owns a Park-Miller stream
+(the reference shares one unlocked stream between threads).
+Stream k of an island with seed s starts at Random(|s| + 1 + k).
+"""
+from __future__ import annotations
+
+import json
+import math
+import time
+
+import numpy as np
+
+# ga.cpp:389-397: -p 1 -> 200, -p 2 -> 1000, otherwise 2000
+MAX_STEPS = {1: 200, 2: 1000}
+
+
+def max_steps_for(problem_type: int) -> int:
+    return MAX_STEPS.get(int(problem_type), 2000)
+
+
+def _fmt(v):
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, (int, np.integer)):
+        return str(int(v))
+    if isinstance(v, float):
+        if math.isnan(v):
+            return "null"
+        if math.isinf(v):
+            return "1e+9999" if v > 0 else "-1e+9999"
+        return "%.17g" % v
+    if isinstance(v, dict):
+        return "{" + ",".join(json.dumps(k) + ":" + _fmt(v[k]) for k in sorted(v)) + "}"
+    if isinstance(v, (list, tuple, np.ndarray)):
+        return "[" + ",".join(_fmt(x) for x in v) + "]"
+    return json.dumps(v)
+
+
+def json_line(obj) -> str:
+    """jsoncpp StreamWriterBuilder with indentation "" (ga.cpp:171): compact,
+    keys sorted (std::map, json/json.h:584), doubles as %.17g (jsoncpp.cpp:4049)."""
+    return _fmt(obj)
+
+
+def stream_seeds(seed: int, first: int, n: int) -> np.ndarray:
+    return (np.arange(first, first + n, dtype=np.int64) + np.int64(abs(int(seed)) + 1)).astype(np.int64)
+
+
+class Island:
+    """One island: population [N] + C child slots, all device-resident."""
+
+    def __init__(self, dp, pop_size: int = 10, children: int = 1, max_steps: int = 200, seed: int = 1,
+                 p_cross: float = 0.8, p_mut: float = 0.5, skip_init_draws: bool = True, device=None,
+                 p1: float = 1.0, p2: float = 1.0, p3: float = 0.0):
+        import torch
+        if not (1 <= children <= pop_size):
+            raise ValueError("need 1 <= children <= pop_size")
+        self.dp, self.N, self.C = dp, int(pop_size), int(children)
+        self.max_steps, self.seed = int(max_steps), int(seed)
+        self.p_cross, self.p_mut, self.skip = float(p_cross), float(p_mut), bool(skip_init_draws)
+        self.p1, self.p2, self.p3 = float(p1), float(p2), float(p3)   # LS move probabilities (Solution.h:61)
+        dev = torch.device("cuda", dp.device if device is None else device)
+        E = dp.E
+
+        def pop(n):
+            return {"slot": torch.zeros((n, E), dtype=torch.uint8, device=dev),
+                    "room": torch.zeros((n, E), dtype=torch.uint8, device=dev),
+                    "hcv": torch.zeros(n, dtype=torch.int32, device=dev),
+                    "scv": torch.zeros(n, dtype=torch.int32, device=dev),
+                    "feasible": torch.zeros(n, dtype=torch.uint8, device=dev),
+                    "penalty": torch.zeros(n, dtype=torch.int32, device=dev)}
+
+        self.pop, self.child = pop(self.N), pop(self.C)
+        self.flags = torch.zeros(self.C, dtype=torch.uint8, device=dev)
+        self.rng_init = torch.from_numpy(stream_seeds(seed, 0, self.N)).to(dev)
+        self.rng_child = torch.from_numpy(stream_seeds(seed, self.N, self.C)).to(dev)
+        self.work = dp.ga_work(self.N)
+        self.generation = 0
+
+    def _evaluate(self, p):
+        self.dp.eval(p["slot"], p["room"], out=(p["hcv"], p["scv"], p["feasible"], p["penalty"]))
+
+    def initialize(self):
+        """ga.cpp:429-434 for every member, then the population is sorted."""
+        p = self.pop
+        self.dp.random_init(self.rng_init, p["slot"], p["room"])
+        self.dp.local_search(p["slot"], p["room"], self.rng_init, self.max_steps, self.p1, self.p2, self.p3)
+        self._evaluate(p)
+        self.dp.ga_replace(p, None, self.work)
+
+    def step(self):
+        """One generation of C children (ga.cpp:543-585)."""
+        c = self.child
+        self.dp.ga_breed(self.pop["slot"], self.pop["room"], self.pop["penalty"], self.rng_child, c["slot"], c["room"],
+                         self.flags, self.p_cross, self.p_mut, self.skip)
+        self.dp.local_search(c["slot"], c["room"], self.rng_child, self.max_steps, self.p1, self.p2, self.p3)
+        self._evaluate(c)
+        self.dp.ga_replace(self.pop, c, self.work)
+        self.generation += 1
+
+    # -- host views ------------------------------------------------------------------
+    def member(self, k: int) -> dict:
+        """deserialised Solution fields of member k (ga.cpp:318-335 payload)."""
+        p = self.pop
+        return {"slot": p["slot"][k].cpu().numpy(), "room": p["room"][k].cpu().numpy(),
+                "feasible": bool(p["feasible"][k].item()), "scv": int(p["scv"][k].item()),
+                "hcv": int(p["hcv"][k].item()), "penalty": int(p["penalty"][k].item())}
+
+    def best_value(self) -> tuple[bool, int]:
+        """(feasible, scv) if feasible else (False, hcv*1e6 + scv) (ga.cpp:191,218,247)."""
+        b = self.member_meta(0)
+        return (True, b[1]) if b[0] else (False, b[2] * 1000000 + b[1])
+
+    def member_meta(self, k: int):
+        p = self.pop
+        return (bool(p["feasible"][k].item()), int(p["scv"][k].item()), int(p["hcv"][k].item()),
+                int(p["penalty"][k].item()))
+
+    # -- migration payloads (device tensors) ---------------------------------------------
+    def pack(self, k: int):
+        """One migrant as a flat uint8 device tensor: slot[E], room[E], meta int32[4]."""
+        import torch
+        p = self.pop
+        meta = torch.stack([p["hcv"][k], p["scv"][k], p["feasible"][k].to(torch.int32), p["penalty"][k]])
+        return torch.cat([p["slot"][k], p["room"][k], meta.view(torch.uint8)])
+
+    def unpack_into(self, pos: int, buf):
+        """deserializeSolution(offset) into population position `pos` (ga.cpp:344-368)."""
+        import torch
+        E = self.dp.E
+        p = self.pop
+        p["slot"][pos].copy_(buf[:E])
+        p["room"][pos].copy_(buf[E:2 * E])
+        meta = buf[2 * E:2 * E + 16].clone().view(torch.int32)
+        p["hcv"][pos] = meta[0]
+        p["scv"][pos] = meta[1]
+        p["feasible"][pos] = meta[2].to(torch.uint8)
+        p["penalty"][pos] = meta[3]
+
+
+class CostLog:
+    """setCurrentCost (ga.cpp:203-228): a logEntry line whenever pop[0] changes the best."""
+
+    def __init__(self, proc_id: int, out, t0: float):
+        self.proc_id, self.out, self.t0 = proc_id, out, t0
+        self.best_scv = 2 ** 31 - 1
+        self.best_eval = 2 ** 31 - 1
+
+    def update(self, island: Island, thread_id: int = 0):
+        feas, scv, hcv, _ = island.member_meta(0)
+        entry = None
+        if feas:
+            if scv != self.best_scv:
+                self.best_scv = scv
+                self.best_eval = scv
+                entry = scv
+        else:
+            ev = hcv * 1000000 + scv
+            if ev < self.best_eval:
+                self.best_eval = ev
+                entry = ev
+        if entry is not None and self.out is not None:
+            t = max(0.0, time.perf_counter() - self.t0)
+            self.out.write(json_line({"logEntry": {"best": entry, "procID": self.proc_id, "threadID": thread_id,
+                                                   "time": t}}) + "\n")

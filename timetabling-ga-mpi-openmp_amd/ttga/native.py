@@ -22,7 +22,7 @@ NUM_SLOTS = 45
 EXPORTS = (
     "tt_problem_create", "tt_problem_destroy", "tt_problem_dims", "tt_problem_derived", "tt_eval",
     "tt_eval_variant", "tt_assign_rooms", "tt_random_init", "tt_crossover", "tt_mutation", "tt_local_search",
-    "tt_device_status", "tt_last_error", "tt_version",
+    "tt_device_status", "tt_last_error", "tt_version", "tt_ga_breed", "tt_ga_work_bytes", "tt_ga_replace",
 )
 
 _lib = None
@@ -57,11 +57,15 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.tt_mutation.argtypes = [vp, vp, vp, vp, i32, vp]
     lib.tt_local_search.argtypes = [vp, vp, vp, vp, i32, i32, dbl, dbl, dbl, vp]
     lib.tt_device_status.argtypes = [vp, vp]
+    lib.tt_ga_breed.argtypes = [vp, vp, vp, vp, i32, vp, i32, dbl, dbl, i32, vp, vp, vp, vp]
+    lib.tt_ga_work_bytes.argtypes = [i32, i32]
+    lib.tt_ga_work_bytes.restype = ctypes.c_size_t
+    lib.tt_ga_replace.argtypes = [vp] * 7 + [i32] + [vp] * 6 + [i32, vp, vp]
     lib.tt_last_error.restype = ctypes.c_char_p
     lib.tt_last_error.argtypes = []
     lib.tt_version.argtypes = []
     for name in EXPORTS:
-        if name not in ("tt_last_error",):
+        if name not in ("tt_last_error", "tt_ga_work_bytes"):
             getattr(lib, name).restype = ctypes.c_int
     if path is None:
         _lib = lib
@@ -176,6 +180,32 @@ class DeviceProblem:
         _check(self.lib, self.lib.tt_local_search(self.handle, slot.data_ptr(), room.data_ptr(), rng.data_ptr(), P,
                                                   int(max_steps), float(p1), float(p2), float(p3),
                                                   self._stream(slot)))
+
+    # -- GA generation primitives ---------------------------------------------------
+    def ga_breed(self, pop_slot, pop_room, pop_penalty, rng, child_slot, child_room, child_flags,
+                 p_cross=0.8, p_mut=0.5, skip_init_draws=True):
+        N = self._pop(pop_slot, pop_room)
+        C = self._pop(child_slot, child_room)
+        self._rng(rng, C)
+        _check(self.lib, self.lib.tt_ga_breed(self.handle, pop_slot.data_ptr(), pop_room.data_ptr(),
+                                              pop_penalty.data_ptr(), N, rng.data_ptr(), C, float(p_cross),
+                                              float(p_mut), int(bool(skip_init_draws)), child_slot.data_ptr(),
+                                              child_room.data_ptr(), child_flags.data_ptr(), self._stream(pop_slot)))
+
+    def ga_work(self, N):
+        import torch
+        return torch.empty(int(self.lib.tt_ga_work_bytes(N, self.E)), dtype=torch.uint8, device="cuda")
+
+    def ga_replace(self, pop, child, work):
+        """pop/child: dicts of device tensors slot, room, hcv, scv, feasible, penalty."""
+        N = self._pop(pop["slot"], pop["room"])
+        C = self._pop(child["slot"], child["room"]) if child is not None else 0
+        c = child or {k: pop[k] for k in pop}
+        _check(self.lib, self.lib.tt_ga_replace(
+            self.handle, pop["slot"].data_ptr(), pop["room"].data_ptr(), pop["hcv"].data_ptr(),
+            pop["scv"].data_ptr(), pop["feasible"].data_ptr(), pop["penalty"].data_ptr(), N,
+            c["slot"].data_ptr(), c["room"].data_ptr(), c["hcv"].data_ptr(), c["scv"].data_ptr(),
+            c["feasible"].data_ptr(), c["penalty"].data_ptr(), C, work.data_ptr(), self._stream(pop["slot"])))
 
     @staticmethod
     def _rng(rng, P):

@@ -23,6 +23,7 @@ run() {
 for s in $STEPS; do
   case $s in
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
+    gatests) run pytest_ga 600 python -u -m pytest tests/test_gpu_ga.py -m gpu -v --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py ;;
     phases) run phases 300 python -u tools/prof_eval.py med 65536 ;;
