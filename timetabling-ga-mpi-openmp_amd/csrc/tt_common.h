@@ -9,6 +9,7 @@ constexpr int kSlots = 45;             // Solution.cpp:52,57
 constexpr int kSlotsPerDay = 9;
 constexpr int kMaxRooms = 64;          // rooms are bitmasks in one 64-bit word
 constexpr int kMaxSlotEvents = 256;    // per-slot event bitsets (4 x 64 bits) in the matcher
+constexpr int kTileWaves = 8;          // waves per workgroup of the eval tile kernel
 
 // slot s is the last of its day (s % 9 == 8): Solution.cpp:94
 constexpr uint64_t kLastSlotMask = (1ull << 8) | (1ull << 17) | (1ull << 26) | (1ull << 35) | (1ull << 44);
@@ -31,6 +32,10 @@ struct DevProblem {
     const uint64_t* cupT;         // [EW64][E] upper-triangle correlation bits, word-major:
                                   //   cupT[w*E+i] bit b <=> corr(i, 64w+b) and 64w+b > i
     const uint64_t* corr64;       // [E][EW64] full eventCorrelations rows (diagonal included)
+    const uint4* wch;             // lane-phase chunk stream of the tile kernel: 8 u16 event ids
+                                  //   per record, students s = w mod kTileWaves for wave w,
+                                  //   bit 15 of id 0 = last chunk of a student (E <= 32767)
+    const int32_t* wch_off;       // [kTileWaves+1] record offsets per wave
     const int32_t* stc_off;       // [S+1] per-student event lists padded to multiples of 8
     const int32_t* stc_ev;        //   padding entries hold E (a sentinel column)
     int32_t* status;              // device status word (tt_device_status)
@@ -51,10 +56,11 @@ __device__ __forceinline__ double pm_next(int64_t& s) {
 // (int)(next() * n): truncation of the fp64 product (Solution.cpp:52, ga.cpp:135)
 __device__ __forceinline__ int pm_pick(int64_t& s, int n) { return (int)__dmul_rn(pm_next(s), (double)n); }
 
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
+// Full-wave sum (every lane active): DPP row shifts + readlane, no LDS round trips.
+__device__ __forceinline__ int wave_sum(int v) { return __reduce_add_sync(~0ull, v); }
+
+// Index of this thread's wave in the workgroup, as a wave-uniform (SGPR) value
+// so that loops and loads driven by it stay scalar.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
 }  // namespace ttga

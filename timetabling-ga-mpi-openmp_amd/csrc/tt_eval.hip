@@ -37,7 +37,7 @@ namespace ttga {
 //    correlated same-slot pairs as popcount(cupT[w][i] & B[slot_i][w]) over the
 //    upper-triangle words (1.6 K word ops per individual at E=400 instead of
 //    13 K neighbour lookups).
-constexpr int kTileWaves = 8;
+
 
 struct TileLayout {
     int SP;           // tile row stride (bytes)
@@ -73,9 +73,9 @@ __global__ __launch_bounds__(64 * kTileWaves) void eval_tile_kernel(DevProblem p
                                                                      uint8_t* __restrict__ feas_out,
                                                                      int32_t* __restrict__ pen_out, int ablate) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int E = pb.E, R = pb.R, S = pb.S;
+    const int E = pb.E, R = pb.R;
     const int EW64 = EWC > 0 ? EWC : pb.EW64;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = wave_id();
     const TileLayout L = tile_layout(E, R);
     // ablate (profiling only, results invalid): 1 skip lane phase, 2 skip wave phase, 4 skip corr words
     const int SP = L.SP;
@@ -127,24 +127,30 @@ __global__ __launch_bounds__(64 * kTileWaves) void eval_tile_kernel(DevProblem p
 
         // ---- lane phase: per-student attendance masks (Solution.cpp:98-137)
         if (!(ablate & 1)) {
+            // this wave's students as one stream of 8-id chunk records; the next
+            // record is loaded while the current one's 8 LDS reads are in flight
             const uint8_t* my = tile + lane * SP;
             int sc = 0;
-            for (int st = wv; st < S; st += kTileWaves) {
-                const int k0 = pb.stc_off[st], k1 = pb.stc_off[st + 1];
+            const int c0 = pb.wch_off[wv], c1 = pb.wch_off[wv + 1];
+            if (c0 < c1) {
+                uint4 cur = pb.wch[c0];
                 uint64_t m = 0;
-                for (int k = k0; k < k1; k += 8) {
-                    int ev[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) ev[j] = pb.stc_ev[k + j];
+                for (int c = c0; c < c1; ++c) {
+                    const uint4 nxt = pb.wch[c + 1 < c1 ? c + 1 : c];
+                    const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
                     uint32_t sl[8];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) sl[j] = my[ev[j]];
+                    for (int j = 0; j < 8; ++j) sl[j] = my[(w[j >> 1] >> (16 * (j & 1))) & 0x7FFFu];
 #pragma unroll
                     for (int j = 0; j < 8; ++j) m |= 1ull << (sl[j] & 63);
-                }
-                sc += __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);
+                    if (cur.x & 0x8000u) {                       // last chunk of a student
+                        sc += __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);
 #pragma unroll
-                for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);
+                        for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);
+                        m = 0;
+                    }
+                    cur = nxt;
+                }
             }
             part[wv * 64 + lane] = sc;
         }

@@ -115,6 +115,23 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         stc_off[s + 1] = (int32_t)stc_ev.size();
     }
     if (stc_ev.empty()) stc_ev.assign(8, E);
+    // per-wave chunk streams for eval_tile's lane phase (students s = w mod kTileWaves)
+    std::vector<uint16_t> wch;
+    std::vector<int32_t> wch_off(kTileWaves + 1, 0);
+    if (E <= 32767) {
+        for (int w = 0; w < kTileWaves; w++) {
+            for (int s = w; s < S; s += kTileWaves) {
+                const int c0 = stc_off[s], c1 = stc_off[s + 1];
+                for (int c = c0; c < c1; c += 8) {
+                    const size_t r = wch.size();
+                    for (int j = 0; j < 8; j++) wch.push_back((uint16_t)stc_ev[c + j]);
+                    if (c + 8 == c1) wch[r] |= 0x8000;
+                }
+            }
+            wch_off[w + 1] = (int32_t)(wch.size() / 8);
+        }
+    }
+    if (wch.empty()) wch.assign(8, 0);
     // possibleRooms (Problem.cpp:130-148): size fits and every required feature present.
     p->poss_bits.assign(E, 0ull);
     for (int i = 0; i < E; i++)
@@ -145,6 +162,8 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         {stc_off.data(), sizeof(int32_t) * stc_off.size(), 0},
         {stc_ev.data(), sizeof(int32_t) * stc_ev.size(), 0},
         {corr64.data(), sizeof(uint64_t) * corr64.size(), 0},
+        {wch.data(), sizeof(uint16_t) * wch.size(), 0},
+        {wch_off.data(), sizeof(int32_t) * wch_off.size(), 0},
     };
     size_t total = 0;
     for (auto& q : parts) { q.off = total; total += (q.bytes + 255) & ~(size_t)255; }
@@ -181,6 +200,8 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     d.stc_off = (const int32_t*)(base + parts[11].off);
     d.stc_ev = (const int32_t*)(base + parts[12].off);
     d.corr64 = (const uint64_t*)(base + parts[13].off);
+    d.wch = (const uint4*)(base + parts[14].off);
+    d.wch_off = (const int32_t*)(base + parts[15].off);
     *out = p;
     return TT_OK;
 }
