@@ -144,7 +144,7 @@ def main():
         value = total / wall_max
         bytes_per_eval = 2 * E + 13                     # u8 slot+room in; i32 hcv,scv,penalty + u8 feasible out
         achieved = bytes_per_eval * P / (kernel_ms * 1e-3) / 1e9
-        variant = args.variant or (1 if E <= 1024 else 2)
+        variant = args.variant or (3 if (E + 63) // 64 <= 7 else 1 if E <= 1024 else 2)
         wkey = f"{args.config}_P{P}_v{variant}"
         tr = pmc_traffic(wkey)
         line = {
@@ -154,7 +154,7 @@ def main():
             "config": {"workload": f"{args.config} instance E={E} R={inst.R} F={inst.F} S={inst.S} (seeded synthetic, "
                                    f"medium01-size), population {P} per GPU, one tt_eval (hcv+scv+feasible+penalty) "
                                    f"per step", "pop_per_gpu": P, "global_pop": P * world,
-                       "kernel": "eval_lanes" if variant == 1 else "eval_block",
+                       "kernel": {1: "eval_tile", 2: "eval_block", 3: "eval_tile4", 4: "eval_tile4_w8"}[variant],
                        "parallelism": f"dp{world} (independent population shards)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": tr,

@@ -70,8 +70,13 @@ int tt_problem_derived(const tt_problem* p, int32_t* student_number, int32_t* co
 int tt_eval(const tt_problem* p, const uint8_t* slot, const uint8_t* room, int P, int32_t* hcv, int32_t* scv,
             uint8_t* feasible, int32_t* penalty, void* stream);
 
-/* tt_eval with an explicit kernel choice: 0 = automatic, 1 = lane-per-individual
- * (E <= 1024), 2 = workgroup-per-individual (any E). For tests and profiling. */
+/* tt_eval with an explicit kernel choice, for tests and profiling:
+ *   0 = automatic (3 when E <= 448, else 1 when the tile fits, else 2),
+ *   1 = eval_tile, 8-wave tile of 64 individuals (E <= 1024),
+ *   2 = eval_block, one workgroup per individual (any E),
+ *   3 = eval_tile4, 4-wave tile, 4 workgroups per CU (E <= 448),
+ *   4 = eval_tile4 with 8 waves (E <= 448).
+ * All variants give identical results. */
 int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const uint8_t* room, int P, int32_t* hcv,
                     int32_t* scv, uint8_t* feasible, int32_t* penalty, int variant, void* stream);
 

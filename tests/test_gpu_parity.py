@@ -54,7 +54,7 @@ def test_derived_matches_reference(problems, name):
     assert np.array_equal(poss, z["ref_possible"])
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
 @pytest.mark.parametrize("name", NAMES)
 @pytest.mark.parametrize("tag,sk,rk", [("canon", "slots", "rooms"), ("rand", "slots", "rand_rooms"),
                                        ("skew", "skew_slots", "skew_rooms"), ("edge", "edge_slots", "edge_rooms"),
@@ -68,9 +68,13 @@ def test_eval_golden(problems, name, tag, sk, rk, variant):
     assert np.array_equal(pen, z[f"eval_{tag}_penalty"])
 
 
-@pytest.mark.parametrize("variant", [1, 2])
-def test_eval_random_vs_oracle(orc, variant):
-    inst = ttga.generate(333, 9, 6, 170, seed=11)      # E not a multiple of 4: byte staging path
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("dims", [(333, 9, 6, 170), (320, 24, 5, 150), (250, 40, 4, 120), (448, 11, 5, 300)],
+                         ids=["E333R9", "E320R24", "E250R40", "E448R11"])
+def test_eval_random_vs_oracle(orc, variant, dims):
+    """Ragged P; E not a multiple of 16 (byte staging path) or of 64; room masks
+    packed with studentNumber (R <= 16), u32 (R <= 32) and u64 (R = 40)."""
+    inst = ttga.generate(*dims, seed=11)
     dp = native.DeviceProblem(inst)
     P = 203                                            # ragged last wave
     slots, _ = ttga.random_slots(ttga.population_seeds(4242, P), inst.E)
@@ -89,7 +93,7 @@ def test_eval_invalid_individual_flagged(problems):
     r = z["rooms"][:3].copy()
     s[1, 7] = 45
     r[2, 3] = inst.R
-    for variant in (1, 2):
+    for variant in (1, 2, 3, 4):
         hcv, scv, feas, pen = (host(t) for t in dp.eval(dev(s), dev(r), variant=variant))
         assert hcv[0] == z["eval_canon_hcv"][0]
         assert list(hcv[1:]) == [-1, -1] and list(pen[1:]) == [-1, -1] and list(feas[1:]) == [0, 0]
@@ -111,10 +115,11 @@ def test_eval_bench_size_properties(orc):
     g = torch.Generator(device="cuda").manual_seed(0)
     slot = torch.randint(0, 45, (P, inst.E), dtype=torch.uint8, device="cuda", generator=g)
     room = dp.assign_rooms(slot)
-    a = [host(t) for t in dp.eval(slot, room, variant=1)]
-    b = [host(t) for t in dp.eval(slot, room, variant=2)]
-    for x, y in zip(a, b):
-        assert np.array_equal(x, y)
+    a = [host(t) for t in dp.eval(slot, room, variant=3)]
+    for v in (1, 2, 4):
+        b = [host(t) for t in dp.eval(slot, room, variant=v)]
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
     hcv, scv, feas, pen = a
     assert np.array_equal(feas.astype(bool), hcv == 0)
     assert np.array_equal(pen, np.where(hcv == 0, scv, 1000000 + hcv))

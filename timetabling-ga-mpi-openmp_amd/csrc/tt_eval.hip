@@ -20,6 +20,7 @@
 //  * eval_block (any E): one 256-thread workgroup per individual; slot
 //    buckets in LDS enumerate only same-slot pairs for the correlation term.
 #include <algorithm>
+#include <type_traits>
 
 #include "tt_internal.h"
 
@@ -250,6 +251,230 @@ __global__ __launch_bounds__(64 * kTileWaves) void eval_tile_kernel(DevProblem p
     }
 }
 
+// ---------------------------------------------------------------- eval_tile4
+// Second-generation tile kernel: NW waves per 64-individual tile, sized so that
+// at E = 400 four workgroups (16 waves) fit one CU and a 65,536-member
+// population is one tile per workgroup.
+//  * lane-phase records come through the scalar cache (s_load_dwordx4 via the
+//    constant address space) from a student-ordered stream; wave w owns a
+//    contiguous student range balanced by record count;
+//  * the wave phase prefetches the next individual's room row while the
+//    current one is scored; cell counters are packed u16 pairs;
+//  * PK selects how a lane keeps possibleRooms/studentNumber of its events:
+//    1 = one packed register (R <= 16, studentNumber < 65536), 2 = u32 mask
+//    (R <= 32), 0 = u64 mask.
+typedef __attribute__((address_space(4))) const uint32_t ConstU32;
+typedef __attribute__((address_space(4))) const int32_t ConstI32;
+
+struct Tile4Layout {
+    int SP, WS;
+    size_t off_wave, off_part, bytes;
+};
+
+__host__ __device__ inline Tile4Layout tile4_layout(int E, int R, int NW) {
+    Tile4Layout L;
+    int sp = (E + 1 + 3) & ~3;
+    if (((sp >> 2) & 1) == 0) sp += 4;
+    L.SP = sp;
+    const int ew64 = (E + 63) / 64;
+    const int cntw = (kSlots * R + 1) / 2;
+    L.WS = (kSlots * ew64 * 8 + cntw * 4 + 15) & ~15;
+    L.off_wave = ((size_t)64 * sp + 15) & ~(size_t)15;
+    L.off_part = L.off_wave + (size_t)NW * L.WS;
+    L.bytes = L.off_part + 4 * (size_t)(NW * 64 + 64);
+    return L;
+}
+
+template <int EWC, int NW, int PK>
+__global__ __launch_bounds__(64 * NW, 16 / NW) void eval_tile4_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
+                                                              const uint8_t* __restrict__ room, int P,
+                                                              int32_t* __restrict__ hcv_out,
+                                                              int32_t* __restrict__ scv_out,
+                                                              uint8_t* __restrict__ feas_out,
+                                                              int32_t* __restrict__ pen_out, int ablate) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int NT = 64 * NW;
+    const int E = pb.E, R = pb.R;
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    const Tile4Layout L = tile4_layout(E, R, NW);
+    const int SP = L.SP;
+    uint8_t* tile = lds;
+    uint8_t* ws = lds + L.off_wave + (size_t)wv * L.WS;
+    uint64_t* B = (uint64_t*)ws;                              // [45][EWC] event bitsets per slot
+    uint32_t* cnt = (uint32_t*)(B + kSlots * EWC);            // [45*R] u16 cell counters, 2 per dword
+    int32_t* part = (int32_t*)(lds + L.off_part);             // [NW][64] scv partials
+    int32_t* hq = part + NW * 64;                             // [64] hcv (or -1)
+    const int tiles = (P + 63) / 64;
+
+    // per-event invariants of this lane's events e = lane + 64 r
+    using PossT = typename std::conditional<PK == 0, uint64_t, uint32_t>::type;
+    uint64_t inv_cup[EWC][EWC];
+    PossT inv_poss[EWC];
+    uint32_t inv_ps[EWC];
+    int inv_sn[EWC];
+#pragma unroll
+    for (int r = 0; r < EWC; ++r) {
+        const int e = lane + 64 * r;
+        const bool ok = e < E;
+        if constexpr (PK == 1) {
+            inv_ps[r] = ok ? ((uint32_t)pb.poss[e] | ((uint32_t)pb.sn[e] << 16)) : 0xFFFFu;
+        } else {
+            inv_poss[r] = ok ? (PossT)pb.poss[e] : (PossT)~0ull;
+            inv_sn[r] = ok ? pb.sn[e] : 0;
+        }
+#pragma unroll
+        for (int w = 0; w < EWC; ++w) inv_cup[r][w] = (w >= r && ok) ? pb.cupT[(size_t)w * E + e] : 0ull;
+    }
+    const ConstU32* rec = (const ConstU32*)pb.sch;
+    const ConstI32* ptab = (const ConstI32*)pb.sch_part;
+    const int pbase = NW == 4 ? kSchPart4 : kSchPart8;
+    const int c0 = ptab[pbase + wv], c1 = ptab[pbase + wv + 1];
+    const bool wide = (E & 15) == 0 && (((uintptr_t)slot) & 15) == 0;
+    const int qpr = E >> 4;
+    const uint32_t qinv = ((1u << 20) + (uint32_t)qpr - 1) / (uint32_t)max(qpr, 1);   // w / qpr for w < 2^12
+
+    for (int tl = blockIdx.x; tl < tiles; tl += gridDim.x) {
+        const long p0 = (long)tl * 64;
+        const int np = (int)min((long)64, (long)P - p0);
+        __syncthreads();
+        // ---- stage the tile's slot rows (+ sentinel column E = slot 63)
+        const uint8_t* src = slot + p0 * E;
+        if (wide) {
+            const uint4* s16 = (const uint4*)src;
+#pragma unroll 2
+            for (int w = threadIdx.x; w < np * qpr; w += NT) {
+                const int r = (int)(((uint32_t)w * qinv) >> 20), c = w - r * qpr;
+                const uint4 v = s16[w];
+                uint32_t* d = (uint32_t*)(tile + r * SP + 16 * c);
+                d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+            }
+        } else {
+#pragma unroll 1
+            for (int r = wv; r < np; r += NW)
+#pragma unroll 1
+                for (int c = lane; c < E; c += 64) tile[r * SP + c] = src[(long)r * E + c];
+        }
+        if (threadIdx.x < 64) tile[threadIdx.x * SP + E] = 63;
+        __syncthreads();
+
+        // ---- lane phase (lane = individual): attendance masks of this wave's students
+        int sc = 0;
+        if (!(ablate & 1) && c0 < c1) {
+            const uint8_t* my = tile + lane * SP;
+            uint32_t cur[4] = {rec[4 * c0], rec[4 * c0 + 1], rec[4 * c0 + 2], rec[4 * c0 + 3]};
+            uint64_t m = 0;
+            for (int c = c0; c < c1; ++c) {
+                const int cn = c + 1 < c1 ? c + 1 : c;
+                const uint32_t nxt[4] = {rec[4 * cn], rec[4 * cn + 1], rec[4 * cn + 2], rec[4 * cn + 3]};
+                const uint32_t* w = cur;
+                uint32_t sl[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) sl[j] = my[(w[j >> 1] >> (16 * (j & 1))) & 0x7FFFu];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) m |= 1ull << (sl[j] & 63);
+                if (cur[0] & 0x8000u) {                                  // last record of a student
+                    sc += __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);   // Solution.cpp:99-117
+#pragma unroll
+                    for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);   // :119-137
+                    m = 0;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+            }
+        }
+        part[wv * 64 + lane] = sc;
+
+        // ---- wave phase (wave = individual): hcv terms + last-slot term
+        const int nq = (ablate & 2) ? 0 : np;
+        uint32_t rvn[EWC];
+#pragma unroll
+        for (int r = 0; r < EWC; ++r) rvn[r] = 0u;
+        if (wv < nq) {
+            const uint8_t* rr = room + (p0 + wv) * E;
+#pragma unroll
+            for (int r = 0; r < EWC; ++r) rvn[r] = lane + 64 * r < E ? rr[lane + 64 * r] : 0u;
+        }
+        for (int q = wv; q < nq; q += NW) {
+            uint32_t rv[EWC], sv[EWC];
+#pragma unroll
+            for (int r = 0; r < EWC; ++r) rv[r] = rvn[r];
+            if (q + NW < nq) {                                          // prefetch the next room row
+                const uint8_t* rr = room + (p0 + q + NW) * E;
+#pragma unroll
+                for (int r = 0; r < EWC; ++r) rvn[r] = lane + 64 * r < E ? rr[lane + 64 * r] : 0u;
+            }
+            for (int c = lane; c < (L.WS >> 4); c += 64) ((uint4*)ws)[c] = make_uint4(0u, 0u, 0u, 0u);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint8_t* rs = tile + q * SP;
+#pragma unroll
+            for (int r = 0; r < EWC; ++r) sv[r] = lane + 64 * r < E ? rs[lane + 64 * r] : 0u;
+            int h = 0, last = 0;
+            bool bad = false;
+#pragma unroll
+            for (int r = 0; r < EWC; ++r) {
+                if (lane + 64 * r < E) {
+                    const uint32_t s = sv[r], ro = rv[r];
+                    if (s >= (uint32_t)kSlots || ro >= (uint32_t)R) {
+                        bad = true;
+                    } else {
+                        atomicOr((unsigned long long*)&B[s * EWC + r], 1ull << lane);
+                        const uint32_t cell = s * R + ro, sh = (cell & 1u) << 4;
+                        const uint32_t old = atomicAdd(&cnt[cell >> 1], 1u << sh);
+                        h += (int)((old >> sh) & 0xFFFFu);                               // Solution.cpp:148-150
+                        const bool last_slot = (kLastSlotMask >> s) & 1ull;
+                        if constexpr (PK == 1) {
+                            h += (int)(((inv_ps[r] >> ro) & 1u) ^ 1u);                  // :155-156
+                            last += last_slot ? (int)(inv_ps[r] >> 16) : 0;             // :93-96
+                        } else {
+                            h += (int)(((inv_poss[r] >> ro) & 1u) ^ 1u);
+                            last += last_slot ? inv_sn[r] : 0;
+                        }
+                    }
+                }
+            }
+            const bool any_bad = __any(bad);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (!any_bad && !(ablate & 4)) {
+#pragma unroll
+                for (int r = 0; r < EWC; ++r) {                                         // :151-153
+                    if (lane + 64 * r < E) {
+                        const uint64_t* brow = B + sv[r] * EWC;
+#pragma unroll
+                        for (int w = r; w < EWC; ++w) h += __popcll(inv_cup[r][w] & brow[w]);
+                    }
+                    if (r & 1) __builtin_amdgcn_sched_barrier(0);   // bound the B words in flight (VGPRs)
+                }
+            }
+            h = wave_sum(h);
+            last = wave_sum(last);
+            if (lane == 0) {
+                hq[q] = any_bad ? -1 : h;
+                part[wv * 64 + q] += last;
+            }
+        }
+        __syncthreads();
+        if (wv == 0 && lane < np) {
+            const long p = p0 + lane;
+            const int h = hq[lane];
+            if (h < 0) {
+                hcv_out[p] = -1; scv_out[p] = -1; feas_out[p] = 0; pen_out[p] = -1;
+            } else {
+                int s2 = 0;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) s2 += part[w * 64 + lane];
+                hcv_out[p] = h;
+                scv_out[p] = s2;
+                feas_out[p] = h == 0 ? 1 : 0;
+                pen_out[p] = h == 0 ? s2 : 1000000 + h;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- eval_block
 constexpr int kBlockThreads = 256;
 
@@ -356,14 +581,17 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
     if (P > 0 && (!hcv || !scv || !feasible || !penalty)) { set_error("null output buffer"); return TT_ERR_INVALID; }
     const int ablate = variant >> 4;   // profiling-only phase switches (tile kernel)
     variant &= 15;
-    if (variant < 0 || variant > 2) { set_error("unknown eval variant"); return TT_ERR_INVALID; }
+    if (variant < 0 || variant > 4) { set_error("unknown eval variant"); return TT_ERR_INVALID; }
     if (P == 0) return TT_OK;
     rc = use_device(p);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     const int E = p->E, R = p->R;
     const TileLayout TL = tile_layout(E, R);
-    if (variant == 0) variant = (E <= 1024 && TL.bytes <= 80 * 1024) ? 1 : 2;
+    if (variant == 0) {
+        if (p->dev.EW64 <= 7 && tile4_layout(E, R, 4).bytes <= 64 * 1024) variant = 3;
+        else variant = (E <= 1024 && TL.bytes <= 80 * 1024) ? 1 : 2;
+    }
     if (variant == 1) {
         if (TL.bytes > 160 * 1024) { set_error("instance too large for the tile kernel"); return TT_ERR_LIMIT; }
         const int tiles = (P + 63) / 64;
@@ -386,6 +614,34 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
             case 7: rc = launch(eval_tile_kernel<7>); break;
             default: rc = launch(eval_tile_kernel<0>); break;
         }
+        if (rc) return rc;
+    } else if (variant == 3 || variant == 4) {
+        const int NW = variant == 3 ? 4 : 8;
+        const Tile4Layout TL4 = tile4_layout(E, R, NW);
+        if (p->dev.EW64 > 7 || TL4.bytes > 160 * 1024) { set_error("instance too large for the tile4 kernel"); return TT_ERR_LIMIT; }
+        const int max_sn = p->student_number.empty() ? 0 : *std::max_element(p->student_number.begin(), p->student_number.end());
+        const int pk = (R <= 16 && max_sn <= 0xFFFF) ? 1 : R <= 32 ? 2 : 0;
+        const int tiles = (P + 63) / 64;
+        auto launch = [&](auto kern) -> int {
+            int per_cu = 0;
+            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, TL4.bytes));
+            const int grid = std::min(tiles, std::max(1, per_cu) * p->num_cus);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NW), TL4.bytes, st, p->dev, slot, room, P, hcv, scv,
+                               feasible, penalty, ablate);
+            return TT_OK;
+        };
+#define TT_T4(EWC)                                                                              \
+    case EWC:                                                                                   \
+        if (NW == 4) rc = pk == 1 ? launch(eval_tile4_kernel<EWC, 4, 1>) : pk == 2 ? launch(eval_tile4_kernel<EWC, 4, 2>) \
+                                  : launch(eval_tile4_kernel<EWC, 4, 0>);                                         \
+        else rc = pk == 1 ? launch(eval_tile4_kernel<EWC, 8, 1>) : pk == 2 ? launch(eval_tile4_kernel<EWC, 8, 2>)     \
+                          : launch(eval_tile4_kernel<EWC, 8, 0>);                                                 \
+        break;
+        switch (p->dev.EW64) {
+            TT_T4(1) TT_T4(2) TT_T4(3) TT_T4(4) TT_T4(5) TT_T4(6) TT_T4(7)
+            default: rc = TT_ERR_LIMIT; break;
+        }
+#undef TT_T4
         if (rc) return rc;
     } else {
         const size_t lds = block_lds_bytes(E, R);

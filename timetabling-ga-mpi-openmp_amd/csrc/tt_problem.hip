@@ -132,6 +132,34 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         }
     }
     if (wch.empty()) wch.assign(8, 0);
+    // the same records in student order, for eval_tile4: wave w of an NW-wave
+    // workgroup takes a contiguous student range, balanced by record count.
+    // sch_part[kSchPart4 + w] (NW = 4) and sch_part[kSchPart8 + w] (NW = 8).
+    std::vector<uint16_t> sch;
+    std::vector<int32_t> stu_rec(S + 1, 0);
+    if (E <= 32767) {
+        for (int s = 0; s < S; s++) {
+            const int c0 = stc_off[s], c1 = stc_off[s + 1];
+            for (int c = c0; c < c1; c += 8) {
+                const size_t r = sch.size();
+                for (int j = 0; j < 8; j++) sch.push_back((uint16_t)stc_ev[c + j]);
+                if (c + 8 == c1) sch[r] |= 0x8000;
+            }
+            stu_rec[s + 1] = (int32_t)(sch.size() / 8);
+        }
+    }
+    std::vector<int32_t> sch_part(kSchPartLen, 0);
+    for (int nw : {4, 8}) {
+        const int base = nw == 4 ? kSchPart4 : kSchPart8;
+        const int total = stu_rec[S];
+        int s = 0;
+        for (int w = 0; w <= nw; w++) {
+            const long target = (long)total * w / nw;
+            while (s < S && stu_rec[s] < target) s++;
+            sch_part[base + w] = w == nw ? total : stu_rec[s];
+        }
+    }
+    if (sch.empty()) sch.assign(8, 0);
     // possibleRooms (Problem.cpp:130-148): size fits and every required feature present.
     p->poss_bits.assign(E, 0ull);
     for (int i = 0; i < E; i++)
@@ -164,6 +192,8 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         {corr64.data(), sizeof(uint64_t) * corr64.size(), 0},
         {wch.data(), sizeof(uint16_t) * wch.size(), 0},
         {wch_off.data(), sizeof(int32_t) * wch_off.size(), 0},
+        {sch.data(), sizeof(uint16_t) * sch.size(), 0},
+        {sch_part.data(), sizeof(int32_t) * sch_part.size(), 0},
     };
     size_t total = 0;
     for (auto& q : parts) { q.off = total; total += (q.bytes + 255) & ~(size_t)255; }
@@ -202,6 +232,8 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     d.corr64 = (const uint64_t*)(base + parts[13].off);
     d.wch = (const uint4*)(base + parts[14].off);
     d.wch_off = (const int32_t*)(base + parts[15].off);
+    d.sch = (const uint4*)(base + parts[16].off);
+    d.sch_part = (const int32_t*)(base + parts[17].off);
     *out = p;
     return TT_OK;
 }
