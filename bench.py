@@ -30,6 +30,8 @@ sys.path.insert(0, str(REPO / "tests"))
 METRIC = json.loads((REPO / "BASELINE.json").read_text())["metric"]
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 POP_PER_GPU = 65536
+KERNELS = {1: "eval_tile", 2: "eval_block", 3: "eval_tile4", 4: "eval_tile4_w8", 5: "eval_tile5_alias",
+           6: "eval_tile5_alias_w8", 7: "eval_tile5", 8: "eval_tile5_w8"}
 
 
 def parse():
@@ -144,7 +146,7 @@ def main():
         value = total / wall_max
         bytes_per_eval = 2 * E + 13                     # u8 slot+room in; i32 hcv,scv,penalty + u8 feasible out
         achieved = bytes_per_eval * P / (kernel_ms * 1e-3) / 1e9
-        variant = args.variant or (3 if (E + 63) // 64 <= 7 else 1 if E <= 1024 else 2)
+        variant = args.variant or dp.eval_variant()
         wkey = f"{args.config}_P{P}_v{variant}"
         tr = pmc_traffic(wkey)
         line = {
@@ -154,7 +156,7 @@ def main():
             "config": {"workload": f"{args.config} instance E={E} R={inst.R} F={inst.F} S={inst.S} (seeded synthetic, "
                                    f"medium01-size), population {P} per GPU, one tt_eval (hcv+scv+feasible+penalty) "
                                    f"per step", "pop_per_gpu": P, "global_pop": P * world,
-                       "kernel": {1: "eval_tile", 2: "eval_block", 3: "eval_tile4", 4: "eval_tile4_w8"}[variant],
+                       "kernel": KERNELS[variant],
                        "parallelism": f"dp{world} (independent population shards)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": tr,

@@ -71,14 +71,20 @@ int tt_eval(const tt_problem* p, const uint8_t* slot, const uint8_t* room, int P
             uint8_t* feasible, int32_t* penalty, void* stream);
 
 /* tt_eval with an explicit kernel choice, for tests and profiling:
- *   0 = automatic (3 when E <= 448, else 1 when the tile fits, else 2),
+ *   0 = automatic (8 when E <= 448, else 1 when the tile fits, else 2),
  *   1 = eval_tile, 8-wave tile of 64 individuals (E <= 1024),
  *   2 = eval_block, one workgroup per individual (any E),
  *   3 = eval_tile4, 4-wave tile, 4 workgroups per CU (E <= 448),
- *   4 = eval_tile4 with 8 waves (E <= 448).
+ *   4 = eval_tile4 with 8 waves (E <= 448),
+ *   5/6 = eval_tile5, 4/8 waves, wave workspaces on top of the tile, u32 cell
+ *         counters (E <= 448),
+ *   7/8 = eval_tile5, 4/8 waves, tile kept, packed u16 cell counters (E <= 448).
  * All variants give identical results. */
 int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const uint8_t* room, int P, int32_t* hcv,
                     int32_t* scv, uint8_t* feasible, int32_t* penalty, int variant, void* stream);
+
+/* The variant tt_eval chooses for this instance (1..8), or -1 for a null handle. */
+int tt_eval_auto_variant(const tt_problem* p);
 
 /* Solution::assignRooms (Solution.cpp:772-891) on every non-empty timeslot in
  * ascending order, events of a slot in ascending index: the max-cardinality

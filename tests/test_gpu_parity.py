@@ -13,6 +13,8 @@ torch = pytest.importorskip("torch")
 from ttga import native  # noqa: E402
 
 NAMES = ["sm", "med", "tight"]
+# tt_eval kernels: 1 eval_tile, 2 eval_block, 3/4 eval_tile4 (4/8 waves), 5-8 eval_tile5
+EVAL_VARIANTS = [1, 2, 3, 4, 5, 6, 7, 8]
 
 
 def load(golden_dir, name):
@@ -54,7 +56,7 @@ def test_derived_matches_reference(problems, name):
     assert np.array_equal(poss, z["ref_possible"])
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("variant", EVAL_VARIANTS)
 @pytest.mark.parametrize("name", NAMES)
 @pytest.mark.parametrize("tag,sk,rk", [("canon", "slots", "rooms"), ("rand", "slots", "rand_rooms"),
                                        ("skew", "skew_slots", "skew_rooms"), ("edge", "edge_slots", "edge_rooms"),
@@ -68,7 +70,7 @@ def test_eval_golden(problems, name, tag, sk, rk, variant):
     assert np.array_equal(pen, z[f"eval_{tag}_penalty"])
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("variant", EVAL_VARIANTS)
 @pytest.mark.parametrize("dims", [(333, 9, 6, 170), (320, 24, 5, 150), (250, 40, 4, 120), (448, 11, 5, 300)],
                          ids=["E333R9", "E320R24", "E250R40", "E448R11"])
 def test_eval_random_vs_oracle(orc, variant, dims):
@@ -93,7 +95,7 @@ def test_eval_invalid_individual_flagged(problems):
     r = z["rooms"][:3].copy()
     s[1, 7] = 45
     r[2, 3] = inst.R
-    for variant in (1, 2, 3, 4):
+    for variant in EVAL_VARIANTS:
         hcv, scv, feas, pen = (host(t) for t in dp.eval(dev(s), dev(r), variant=variant))
         assert hcv[0] == z["eval_canon_hcv"][0]
         assert list(hcv[1:]) == [-1, -1] and list(pen[1:]) == [-1, -1] and list(feas[1:]) == [0, 0]
@@ -116,7 +118,7 @@ def test_eval_bench_size_properties(orc):
     slot = torch.randint(0, 45, (P, inst.E), dtype=torch.uint8, device="cuda", generator=g)
     room = dp.assign_rooms(slot)
     a = [host(t) for t in dp.eval(slot, room, variant=3)]
-    for v in (1, 2, 4):
+    for v in (v for v in EVAL_VARIANTS if v != 3):
         b = [host(t) for t in dp.eval(slot, room, variant=v)]
         for x, y in zip(a, b):
             assert np.array_equal(x, y)

@@ -475,6 +475,294 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void eval_tile4_kernel(DevProblem
     }
 }
 
+// ---------------------------------------------------------------- eval_tile5
+// Third-generation tile kernel. Same two phases as eval_tile4, rearranged so
+// that the LDS holds either the tile or the wave workspaces, never both:
+//  * lane phase as eval_tile4 (8-padded per-student records through the scalar
+//    cache; a back-to-back record stream with per-entry end flags measured
+//    slower: its uniform per-entry branches serialise the mask updates);
+//  * after a workgroup barrier the tile is dead and its bytes become the
+//    per-wave workspaces; the wave phase reads each individual's slot and
+//    room rows straight from global memory (L2-hot: the staging loads just
+//    touched them), one individual ahead;
+//  * an individual with an invalid gene is detected from registers before any
+//    LDS work (its outputs are the -1 sentinels anyway); the valid path has
+//    no per-event branches except on the last, partial event word;
+//  * CNT32: u32 cell counters (address = one mad); otherwise packed u16 pairs;
+//  * B rows are read with single ds_read_b64 (lds_row_b64 below).
+
+// LDS byte address of a pointer into dynamic shared memory.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// N consecutive 64-bit LDS words at byte address addr, as N single
+// ds_read_b64 (the compiler would pair them into ds_read2_b64) with the wait
+// in the same asm block, so the results are defined when it ends.
+#define TT_RD(k, o) "ds_read_b64 %" #k ", %" #o " offset:" #k "*8\n"
+template <int N>
+__device__ __forceinline__ void lds_row_b64(uint32_t addr, uint64_t* v) {
+    static_assert(N >= 1 && N <= 7, "1..7 words");
+    uint64_t d[7];
+    if constexpr (N == 7)
+        asm volatile(TT_RD(0, 7) TT_RD(1, 7) TT_RD(2, 7) TT_RD(3, 7) TT_RD(4, 7) TT_RD(5, 7) TT_RD(6, 7) "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]), "=&v"(d[6])
+                     : "v"(addr) : "memory");
+    else if constexpr (N == 6)
+        asm volatile(TT_RD(0, 6) TT_RD(1, 6) TT_RD(2, 6) TT_RD(3, 6) TT_RD(4, 6) TT_RD(5, 6) "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]) : "v"(addr) : "memory");
+    else if constexpr (N == 5)
+        asm volatile(TT_RD(0, 5) TT_RD(1, 5) TT_RD(2, 5) TT_RD(3, 5) TT_RD(4, 5) "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]) : "v"(addr) : "memory");
+    else if constexpr (N == 4)
+        asm volatile(TT_RD(0, 4) TT_RD(1, 4) TT_RD(2, 4) TT_RD(3, 4) "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]) : "v"(addr) : "memory");
+    else if constexpr (N == 3)
+        asm volatile(TT_RD(0, 3) TT_RD(1, 3) TT_RD(2, 3) "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]) : "v"(addr) : "memory");
+    else if constexpr (N == 2)
+        asm volatile(TT_RD(0, 2) TT_RD(1, 2) "s_waitcnt lgkmcnt(0)" : "=&v"(d[0]), "=&v"(d[1]) : "v"(addr) : "memory");
+    else
+        asm volatile(TT_RD(0, 1) "s_waitcnt lgkmcnt(0)" : "=&v"(d[0]) : "v"(addr) : "memory");
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = d[k];
+}
+#undef TT_RD
+
+// Correlated same-slot pairs of the lane's events (word R onwards):
+// h += popcount(cupT upper words & B[slot] words), one asm row read per event word.
+template <int R, int EWC>
+__device__ __forceinline__ void corr_words(uint32_t bbase, const uint32_t* sv, const uint64_t (*cup)[EWC], int lane,
+                                           int E, bool last_partial, int& h) {
+    if constexpr (R < EWC) {
+        if (R < EWC - 1 || !last_partial || lane + 64 * R < E) {
+            uint64_t bw[EWC - R];
+            lds_row_b64<EWC - R>(bbase + sv[R] * (uint32_t)(EWC * 8) + 8 * R, bw);
+#pragma unroll
+            for (int w = R; w < EWC; ++w) h += __popcll(cup[R][w] & bw[w - R]);
+        }
+        corr_words<R + 1, EWC>(bbase, sv, cup, lane, E, last_partial, h);
+    }
+}
+
+struct Tile5Layout {
+    int SP, WS;
+    size_t off_ws, off_part, bytes;
+};
+
+__host__ __device__ inline Tile5Layout tile5_layout(int E, int R, int NW, bool cnt32, bool alias) {
+    Tile5Layout L;
+    int sp = (E + 1 + 3) & ~3;
+    if (((sp >> 2) & 1) == 0) sp += 4;
+    L.SP = sp;
+    const int ew64 = (E + 63) / 64;
+    const int cntb = cnt32 ? kSlots * R * 4 : ((kSlots * R + 1) / 2) * 4;
+    L.WS = (kSlots * ew64 * 8 + cntb + 15) & ~15;
+    L.off_ws = alias ? 0 : (((size_t)64 * sp + 15) & ~(size_t)15);
+    const size_t uni = alias ? std::max((size_t)64 * sp, (size_t)NW * L.WS) : L.off_ws + (size_t)NW * L.WS;
+    L.off_part = (uni + 15) & ~(size_t)15;
+    L.bytes = L.off_part + 4 * (size_t)(NW * 64 + 64);
+    return L;
+}
+
+template <int EWC, int NW, bool CNT32, int PK, bool ALIAS>
+__global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
+                                                              const uint8_t* __restrict__ room, int P,
+                                                              int32_t* __restrict__ hcv_out,
+                                                              int32_t* __restrict__ scv_out,
+                                                              uint8_t* __restrict__ feas_out,
+                                                              int32_t* __restrict__ pen_out, int ablate) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int NT = 64 * NW;
+    const int E = pb.E, R = pb.R;
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    const Tile5Layout L = tile5_layout(E, R, NW, CNT32, ALIAS);
+    const int SP = L.SP;
+    uint8_t* tile = lds;
+    uint8_t* ws = lds + L.off_ws + (size_t)wv * L.WS;         // ALIAS: on top of the dead tile
+    uint64_t* B = (uint64_t*)ws;                              // [45][EWC] event bitsets per slot
+    uint32_t* cnt = (uint32_t*)(B + kSlots * EWC);            // cell counters
+    int32_t* part = (int32_t*)(lds + L.off_part);             // [NW][64] scv partials
+    int32_t* hq = part + NW * 64;                             // [64] hcv (or -1)
+    const int tiles = (P + 63) / 64;
+    const bool last_partial = E < 64 * EWC;                   // lanes of word EWC-1 beyond E
+
+    // PK as in eval_tile4: 1 = possibleRooms | studentNumber << 16 in one register
+    // (R <= 16, studentNumber < 65536), 2 = u32 mask (R <= 32), 0 = u64 mask
+    using PossT = typename std::conditional<PK == 0, uint64_t, uint32_t>::type;
+    uint64_t inv_cup[EWC][EWC];
+    PossT inv_poss[EWC];
+    uint32_t inv_ps[EWC];
+    int inv_sn[EWC];
+#pragma unroll
+    for (int r = 0; r < EWC; ++r) {
+        const int e = lane + 64 * r;
+        const bool ok = e < E;
+        if constexpr (PK == 1) {
+            inv_ps[r] = ok ? ((uint32_t)pb.poss[e] | ((uint32_t)pb.sn[e] << 16)) : 0xFFFFu;
+        } else {
+            inv_poss[r] = ok ? (PossT)pb.poss[e] : (PossT)~0ull;
+            inv_sn[r] = ok ? pb.sn[e] : 0;
+        }
+#pragma unroll
+        for (int w = 0; w < EWC; ++w) inv_cup[r][w] = (w >= r && ok) ? pb.cupT[(size_t)w * E + e] : 0ull;
+    }
+    const ConstU32* rec = (const ConstU32*)pb.sch;
+    const ConstI32* ptab = (const ConstI32*)pb.sch_part;
+    const int pbase = NW == 4 ? kSchPart4 : kSchPart8;
+    const int c0 = ptab[pbase + wv], c1 = ptab[pbase + wv + 1];
+    const bool wide = (E & 15) == 0 && (((uintptr_t)slot) & 15) == 0;
+    const int qpr = E >> 4;
+    const uint32_t qinv = ((1u << 20) + (uint32_t)qpr - 1) / (uint32_t)max(qpr, 1);
+
+    for (int tl = blockIdx.x; tl < tiles; tl += gridDim.x) {
+        const long p0 = (long)tl * 64;
+        const int np = (int)min((long)64, (long)P - p0);
+        __syncthreads();
+        // ---- stage the tile's slot rows (+ sentinel column E = slot 63)
+        const uint8_t* src = slot + p0 * E;
+        if (wide) {
+            const uint4* s16 = (const uint4*)src;
+#pragma unroll 2
+            for (int w = threadIdx.x; w < np * qpr; w += NT) {
+                const int r = (int)(((uint32_t)w * qinv) >> 20), c = w - r * qpr;
+                const uint4 v = s16[w];
+                uint32_t* d = (uint32_t*)(tile + r * SP + 16 * c);
+                d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+            }
+        } else {
+#pragma unroll 1
+            for (int r = wv; r < np; r += NW)
+#pragma unroll 1
+                for (int c = lane; c < E; c += 64) tile[r * SP + c] = src[(long)r * E + c];
+        }
+        if (threadIdx.x < 64) tile[threadIdx.x * SP + E] = 63;
+        __syncthreads();
+
+        // ---- lane phase (lane = individual): attendance masks of this wave's students
+        int sc = 0;
+        if (!(ablate & 1) && c0 < c1) {
+            const uint8_t* my = tile + lane * SP;
+            uint32_t cur[4] = {rec[4 * c0], rec[4 * c0 + 1], rec[4 * c0 + 2], rec[4 * c0 + 3]};
+            uint64_t m = 0;
+            for (int c = c0; c < c1; ++c) {
+                const int cn = c + 1 < c1 ? c + 1 : c;
+                const uint32_t nxt[4] = {rec[4 * cn], rec[4 * cn + 1], rec[4 * cn + 2], rec[4 * cn + 3]};
+                uint32_t sl[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) sl[j] = my[(cur[j >> 1] >> (16 * (j & 1))) & 0x7FFFu];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) m |= 1ull << (sl[j] & 63);
+                if (cur[0] & 0x8000u) {                                  // last record of a student
+                    sc += __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);   // Solution.cpp:99-117
+#pragma unroll
+                    for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);   // :119-137
+                    m = 0;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+            }
+        }
+        part[wv * 64 + lane] = sc;
+        if constexpr (ALIAS) __syncthreads();                           // the tile is dead from here
+
+        // ---- wave phase (wave = individual): hcv terms + last-slot term
+        const int nq = (ablate & 2) ? 0 : np;
+        // one row (slot rows if ALIAS, else room rows) is prefetched one individual ahead
+        uint32_t pfn[EWC];
+        auto load_row = [&](const uint8_t* base, int q, uint32_t* dst) {
+            const uint8_t* rr = base + (p0 + q) * E;
+#pragma unroll
+            for (int r = 0; r < EWC; ++r)
+                dst[r] = (!last_partial || r < EWC - 1 || lane + 64 * r < E) ? rr[lane + 64 * r] : 0u;
+        };
+        const uint8_t* pf_src = ALIAS ? slot : room;
+        if (wv < nq) load_row(pf_src, wv, pfn);
+        for (int q = wv; q < nq; q += NW) {
+            uint32_t rv[EWC], sv[EWC];
+            if constexpr (ALIAS) {
+#pragma unroll
+                for (int r = 0; r < EWC; ++r) sv[r] = pfn[r];
+                load_row(room, q, rv);
+            } else {
+#pragma unroll
+                for (int r = 0; r < EWC; ++r) rv[r] = pfn[r];
+                const uint8_t* rs = tile + q * SP;
+#pragma unroll
+                for (int r = 0; r < EWC; ++r)
+                    sv[r] = (!last_partial || r < EWC - 1 || lane + 64 * r < E) ? rs[lane + 64 * r] : 0u;
+            }
+            if (q + NW < nq) load_row(pf_src, q + NW, pfn);             // next individual
+            // an invalid gene anywhere -> sentinel outputs; decided from registers
+            uint32_t smax = 0, rmax = 0;
+#pragma unroll
+            for (int r = 0; r < EWC; ++r) { smax = max(smax, sv[r]); rmax = max(rmax, rv[r]); }
+            const bool any_bad = __any(smax >= (uint32_t)kSlots || rmax >= (uint32_t)R);
+            int h = 0, last = 0;
+            if (!any_bad) {
+                for (int c = lane; c < (L.WS >> 4); c += 64) ((uint4*)ws)[c] = make_uint4(0u, 0u, 0u, 0u);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                for (int r = 0; r < EWC; ++r) {
+                    if (r < EWC - 1 || !last_partial || lane + 64 * r < E) {
+                        const uint32_t s = sv[r], ro = rv[r];
+                        atomicOr((unsigned long long*)&B[s * EWC + r], 1ull << lane);
+                        const uint32_t cell = s * (uint32_t)R + ro;
+                        if constexpr (CNT32) {
+                            h += (int)atomicAdd(&cnt[cell], 1u);                        // Solution.cpp:148-150
+                        } else {
+                            const uint32_t sh = (cell & 1u) << 4;
+                            h += (int)((atomicAdd(&cnt[cell >> 1], 1u << sh) >> sh) & 0xFFFFu);
+                        }
+                        const bool last_slot = (kLastSlotMask >> s) & 1ull;
+                        if constexpr (PK == 1) {
+                            h += (int)(((inv_ps[r] >> ro) & 1u) ^ 1u);                  // :155-156
+                            last += last_slot ? (int)(inv_ps[r] >> 16) : 0;             // :93-96
+                        } else {
+                            h += (int)(((inv_poss[r] >> ro) & 1u) ^ 1u);
+                            last += last_slot ? inv_sn[r] : 0;
+                        }
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (!(ablate & 4)) {
+                    // B-row words by single ds_read_b64 (2 LDS cycles per 512 B, 64 banks),
+                    // not the ds_read2_b64 pairs the compiler forms (8 cycles per 1 KiB, 32 banks)
+                    corr_words<0, EWC>(lds_addr(B), sv, inv_cup, lane, E, last_partial, h);   // :151-153
+                }
+                h = wave_sum(h);
+                last = wave_sum(last);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            if (lane == 0) {
+                hq[q] = any_bad ? -1 : h;
+                part[wv * 64 + q] += last;
+            }
+        }
+        __syncthreads();
+        if (wv == 0 && lane < np) {
+            const long p = p0 + lane;
+            const int h = hq[lane];
+            if (h < 0) {
+                hcv_out[p] = -1; scv_out[p] = -1; feas_out[p] = 0; pen_out[p] = -1;
+            } else {
+                int s2 = 0;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) s2 += part[w * 64 + lane];
+                hcv_out[p] = h;
+                scv_out[p] = s2;
+                feas_out[p] = h == 0 ? 1 : 0;
+                pen_out[p] = h == 0 ? s2 : 1000000 + h;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- eval_block
 constexpr int kBlockThreads = 256;
 
@@ -574,6 +862,16 @@ static size_t block_lds_bytes(int E, int R) {
 
 using namespace ttga;
 
+// The kernel tt_eval runs for this instance (see tt_eval_variant).
+static int auto_variant(const tt_problem* p) {
+    const int E = p->E, R = p->R;
+    if (p->dev.EW64 <= 7 && E <= 32767 && tile5_layout(E, R, 8, false, false).bytes <= 80 * 1024) return 8;
+    if (p->dev.EW64 <= 7 && tile4_layout(E, R, 4).bytes <= 64 * 1024) return 3;
+    return (E <= 1024 && tile_layout(E, R).bytes <= 80 * 1024) ? 1 : 2;
+}
+
+extern "C" int tt_eval_auto_variant(const tt_problem* p) { return p ? auto_variant(p) : -1; }
+
 extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const uint8_t* room, int P, int32_t* hcv,
                                int32_t* scv, uint8_t* feasible, int32_t* penalty, int variant, void* stream) {
     int rc = check_pop_args(p, P, slot, room);
@@ -581,17 +879,14 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
     if (P > 0 && (!hcv || !scv || !feasible || !penalty)) { set_error("null output buffer"); return TT_ERR_INVALID; }
     const int ablate = variant >> 4;   // profiling-only phase switches (tile kernel)
     variant &= 15;
-    if (variant < 0 || variant > 4) { set_error("unknown eval variant"); return TT_ERR_INVALID; }
+    if (variant < 0 || variant > 8) { set_error("unknown eval variant"); return TT_ERR_INVALID; }
     if (P == 0) return TT_OK;
     rc = use_device(p);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     const int E = p->E, R = p->R;
     const TileLayout TL = tile_layout(E, R);
-    if (variant == 0) {
-        if (p->dev.EW64 <= 7 && tile4_layout(E, R, 4).bytes <= 64 * 1024) variant = 3;
-        else variant = (E <= 1024 && TL.bytes <= 80 * 1024) ? 1 : 2;
-    }
+    if (variant == 0) variant = auto_variant(p);
     if (variant == 1) {
         if (TL.bytes > 160 * 1024) { set_error("instance too large for the tile kernel"); return TT_ERR_LIMIT; }
         const int tiles = (P + 63) / 64;
@@ -642,6 +937,42 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
             default: rc = TT_ERR_LIMIT; break;
         }
 #undef TT_T4
+        if (rc) return rc;
+    } else if (variant >= 5 && variant <= 8) {
+        // 5/6: eval_tile5 with 4/8 waves, workspaces aliased on the tile, u32 cell
+        // counters; 7/8: tile kept for the wave phase, packed u16 counters
+        const int NW = (variant == 5 || variant == 7) ? 4 : 8;
+        const bool c32 = variant <= 6;          // u32 counters live on top of the dead tile
+        const Tile5Layout TL5 = tile5_layout(E, R, NW, c32, c32);
+        if (p->dev.EW64 > 7 || TL5.bytes > 160 * 1024 || E > 32767) {
+            set_error("instance too large for the tile5 kernel");
+            return TT_ERR_LIMIT;
+        }
+        const int max_sn = p->student_number.empty() ? 0 : *std::max_element(p->student_number.begin(), p->student_number.end());
+        const int pk = (R <= 16 && max_sn <= 0xFFFF) ? 1 : R <= 32 ? 2 : 0;
+        const int tiles = (P + 63) / 64;
+        auto launch = [&](auto kern) -> int {
+            int per_cu = 0;
+            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, TL5.bytes));
+            const int grid = std::min(tiles, std::max(1, per_cu) * p->num_cus);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NW), TL5.bytes, st, p->dev, slot, room, P, hcv, scv,
+                               feasible, penalty, ablate);
+            return TT_OK;
+        };
+#define TT_T5N(EWC, NWV, C)                                                                          \
+    rc = pk == 1 ? launch(eval_tile5_kernel<EWC, NWV, C, 1, C>) : pk == 2 ? launch(eval_tile5_kernel<EWC, NWV, C, 2, C>) \
+                 : launch(eval_tile5_kernel<EWC, NWV, C, 0, C>);
+#define TT_T5(EWC)                                                      \
+    case EWC:                                                           \
+        if (NW == 4) { if (c32) { TT_T5N(EWC, 4, true) } else { TT_T5N(EWC, 4, false) } } \
+        else { if (c32) { TT_T5N(EWC, 8, true) } else { TT_T5N(EWC, 8, false) } }         \
+        break;
+        switch (p->dev.EW64) {
+            TT_T5(1) TT_T5(2) TT_T5(3) TT_T5(4) TT_T5(5) TT_T5(6) TT_T5(7)
+            default: rc = TT_ERR_LIMIT; break;
+        }
+#undef TT_T5
+#undef TT_T5N
         if (rc) return rc;
     } else {
         const size_t lds = block_lds_bytes(E, R);

@@ -23,6 +23,7 @@ EXPORTS = (
     "tt_problem_create", "tt_problem_destroy", "tt_problem_dims", "tt_problem_derived", "tt_eval",
     "tt_eval_variant", "tt_assign_rooms", "tt_random_init", "tt_crossover", "tt_mutation", "tt_local_search",
     "tt_device_status", "tt_last_error", "tt_version", "tt_ga_breed", "tt_ga_work_bytes", "tt_ga_replace",
+    "tt_eval_auto_variant",
 )
 
 _lib = None
@@ -57,6 +58,7 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.tt_mutation.argtypes = [vp, vp, vp, vp, i32, vp]
     lib.tt_local_search.argtypes = [vp, vp, vp, vp, i32, i32, dbl, dbl, dbl, vp]
     lib.tt_device_status.argtypes = [vp, vp]
+    lib.tt_eval_auto_variant.argtypes = [vp]
     lib.tt_ga_breed.argtypes = [vp, vp, vp, vp, i32, vp, i32, dbl, dbl, i32, vp, vp, vp, vp]
     lib.tt_ga_work_bytes.argtypes = [i32, i32]
     lib.tt_ga_work_bytes.restype = ctypes.c_size_t
@@ -113,6 +115,10 @@ class DeviceProblem:
         poss = np.zeros((self.E, self.R), np.int32)
         _check(self.lib, self.lib.tt_problem_derived(self.handle, _np_ptr(sn), _np_ptr(corr), _np_ptr(poss)))
         return sn, corr, poss
+
+    def eval_variant(self) -> int:
+        """The kernel tt_eval runs for this instance (tt_eval_variant numbering)."""
+        return int(self.lib.tt_eval_auto_variant(self.handle))
 
     def status(self) -> int:
         v = ctypes.c_int32(0)

@@ -1,0 +1,9 @@
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out/ev1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -k "eval" --timeout 120 --timeout-method thread > gpurun_out/ev1/pytest.log 2>&1; rc=$?
+tail -5 gpurun_out/ev1/pytest.log
+[ $rc -ge 124 ] && exit $rc
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 python -u tools/eval_variants.py med 65536 3,5,6,7,8,19,21,23,35,37,39 > gpurun_out/ev1/variants.json 2>gpurun_out/ev1/err.log
+rc=$?; cat gpurun_out/ev1/variants.json; exit $rc
