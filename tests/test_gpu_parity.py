@@ -13,8 +13,8 @@ torch = pytest.importorskip("torch")
 from ttga import native  # noqa: E402
 
 NAMES = ["sm", "med", "tight"]
-# tt_eval kernels: 1 eval_tile, 2 eval_block, 3/4 eval_tile4 (4/8 waves), 5-8 eval_tile5
-EVAL_VARIANTS = [1, 2, 3, 4, 5, 6, 7, 8]
+# tt_eval kernels: 1 eval_tile, 2 eval_block, 3/4 eval_tile4 (4/8 waves), 5-8 eval_tile5, 9/10 split
+EVAL_VARIANTS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10]
 
 
 def load(golden_dir, name):

@@ -763,6 +763,196 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
     }
 }
 
+// ---------------------------------------------------------------- eval_split
+// The two phases of eval_tile5 as two launches on the same stream, so that
+// each runs at the occupancy its own registers and LDS allow instead of the
+// fused kernel's common minimum (128 VGPRs for the register-resident
+// correlation words, a 26 KB tile per 64 individuals):
+//  * eval_lanes_kernel (lane = individual): stages a tile, builds the
+//    attendance masks of the wave's student range and writes the per-student
+//    scv part (>2 in a row + single class) of each individual to scv_out;
+//  * eval_waves_kernel (wave = individual, no tile, no workgroup barrier):
+//    slot and room rows straight from global memory (one individual ahead),
+//    the hcv terms and the last-slot term; it adds the latter to scv_out and
+//    writes the final four outputs.
+template <int NWL>
+__global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, const uint8_t* __restrict__ slot, int P,
+                                                              int32_t* __restrict__ scv_part) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int NT = 64 * NWL;
+    const int E = pb.E;
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    int sp = (E + 1 + 3) & ~3;
+    if (((sp >> 2) & 1) == 0) sp += 4;
+    const int SP = sp;
+    uint8_t* tile = lds;
+    int32_t* part = (int32_t*)(lds + (((size_t)64 * SP + 15) & ~(size_t)15));   // [NWL][64]
+    const int tiles = (P + 63) / 64;
+    const ConstU32* rec = (const ConstU32*)pb.sch;
+    const ConstI32* ptab = (const ConstI32*)pb.sch_part;
+    const int pbase = NWL == 4 ? kSchPart4 : kSchPart8;
+    const int c0 = ptab[pbase + wv], c1 = ptab[pbase + wv + 1];
+    const bool wide = (E & 15) == 0 && (((uintptr_t)slot) & 15) == 0;
+    const int qpr = E >> 4;
+    const uint32_t qinv = ((1u << 20) + (uint32_t)qpr - 1) / (uint32_t)max(qpr, 1);
+
+    for (int tl = blockIdx.x; tl < tiles; tl += gridDim.x) {
+        const long p0 = (long)tl * 64;
+        const int np = (int)min((long)64, (long)P - p0);
+        __syncthreads();
+        const uint8_t* src = slot + p0 * E;
+        if (wide) {
+            const uint4* s16 = (const uint4*)src;
+#pragma unroll 2
+            for (int w = threadIdx.x; w < np * qpr; w += NT) {
+                const int r = (int)(((uint32_t)w * qinv) >> 20), c = w - r * qpr;
+                const uint4 v = s16[w];
+                uint32_t* d = (uint32_t*)(tile + r * SP + 16 * c);
+                d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+            }
+        } else {
+#pragma unroll 1
+            for (int r = wv; r < np; r += NWL)
+#pragma unroll 1
+                for (int c = lane; c < E; c += 64) tile[r * SP + c] = src[(long)r * E + c];
+        }
+        if (threadIdx.x < 64) tile[threadIdx.x * SP + E] = 63;
+        __syncthreads();
+        int sc = 0;
+        if (c0 < c1) {
+            const uint8_t* my = tile + lane * SP;
+            uint32_t cur[4] = {rec[4 * c0], rec[4 * c0 + 1], rec[4 * c0 + 2], rec[4 * c0 + 3]};
+            uint64_t m = 0;
+            for (int c = c0; c < c1; ++c) {
+                const int cn = c + 1 < c1 ? c + 1 : c;
+                const uint32_t nxt[4] = {rec[4 * cn], rec[4 * cn + 1], rec[4 * cn + 2], rec[4 * cn + 3]};
+                uint32_t sl[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) sl[j] = my[(cur[j >> 1] >> (16 * (j & 1))) & 0x7FFFu];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) m |= 1ull << (sl[j] & 63);
+                if (cur[0] & 0x8000u) {                                  // last record of a student
+                    sc += __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);   // Solution.cpp:99-117
+#pragma unroll
+                    for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);   // :119-137
+                    m = 0;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+            }
+        }
+        part[wv * 64 + lane] = sc;
+        __syncthreads();
+        if (wv == 0 && lane < np) {
+            int s2 = 0;
+#pragma unroll
+            for (int w = 0; w < NWL; ++w) s2 += part[w * 64 + lane];
+            scv_part[p0 + lane] = s2;
+        }
+    }
+}
+
+constexpr int kWavesWG = 4;   // waves per workgroup of eval_waves_kernel
+
+template <int EWC, int PK>
+__global__ __launch_bounds__(64 * kWavesWG, 4) void eval_waves_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
+                                                                      const uint8_t* __restrict__ room, int P,
+                                                                      int32_t* __restrict__ hcv_out,
+                                                                      int32_t* __restrict__ scv_io,
+                                                                      uint8_t* __restrict__ feas_out,
+                                                                      int32_t* __restrict__ pen_out, int WS) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int E = pb.E, R = pb.R;
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    uint8_t* ws = lds + (size_t)wv * WS;
+    uint64_t* B = (uint64_t*)ws;                              // [45][EWC] event bitsets per slot
+    uint32_t* cnt = (uint32_t*)(B + kSlots * EWC);            // packed u16 cell counters
+    const bool last_partial = E < 64 * EWC;
+
+    using PossT = typename std::conditional<PK == 0, uint64_t, uint32_t>::type;
+    uint64_t inv_cup[EWC][EWC];
+    PossT inv_poss[EWC];
+    uint32_t inv_ps[EWC];
+    int inv_sn[EWC];
+#pragma unroll
+    for (int r = 0; r < EWC; ++r) {
+        const int e = lane + 64 * r;
+        const bool ok = e < E;
+        if constexpr (PK == 1) {
+            inv_ps[r] = ok ? ((uint32_t)pb.poss[e] | ((uint32_t)pb.sn[e] << 16)) : 0xFFFFu;
+        } else {
+            inv_poss[r] = ok ? (PossT)pb.poss[e] : (PossT)~0ull;
+            inv_sn[r] = ok ? pb.sn[e] : 0;
+        }
+#pragma unroll
+        for (int w = 0; w < EWC; ++w) inv_cup[r][w] = (w >= r && ok) ? pb.cupT[(size_t)w * E + e] : 0ull;
+    }
+    auto load_row = [&](const uint8_t* base, long q, uint32_t* dst) {
+        const uint8_t* rr = base + q * E;
+#pragma unroll
+        for (int r = 0; r < EWC; ++r)
+            dst[r] = (!last_partial || r < EWC - 1 || lane + 64 * r < E) ? rr[lane + 64 * r] : 0u;
+    };
+    const long GW = (long)gridDim.x * kWavesWG;
+    long q = (long)blockIdx.x * kWavesWG + wv;
+    uint32_t svn[EWC], rvn[EWC];
+    if (q < P) { load_row(slot, q, svn); load_row(room, q, rvn); }
+    for (; q < P; q += GW) {
+        uint32_t sv[EWC], rv[EWC];
+#pragma unroll
+        for (int r = 0; r < EWC; ++r) { sv[r] = svn[r]; rv[r] = rvn[r]; }
+        if (q + GW < P) { load_row(slot, q + GW, svn); load_row(room, q + GW, rvn); }
+        uint32_t smax = 0, rmax = 0;
+#pragma unroll
+        for (int r = 0; r < EWC; ++r) { smax = max(smax, sv[r]); rmax = max(rmax, rv[r]); }
+        const bool any_bad = __any(smax >= (uint32_t)kSlots || rmax >= (uint32_t)R);
+        int h = 0, last = 0;
+        if (!any_bad) {
+            for (int c = lane; c < (WS >> 4); c += 64) ((uint4*)ws)[c] = make_uint4(0u, 0u, 0u, 0u);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int r = 0; r < EWC; ++r) {
+                if (r < EWC - 1 || !last_partial || lane + 64 * r < E) {
+                    const uint32_t s = sv[r], ro = rv[r];
+                    atomicOr((unsigned long long*)&B[s * EWC + r], 1ull << lane);
+                    const uint32_t cell = s * (uint32_t)R + ro, sh = (cell & 1u) << 4;
+                    h += (int)((atomicAdd(&cnt[cell >> 1], 1u << sh) >> sh) & 0xFFFFu);   // Solution.cpp:148-150
+                    const bool last_slot = (kLastSlotMask >> s) & 1ull;
+                    if constexpr (PK == 1) {
+                        h += (int)(((inv_ps[r] >> ro) & 1u) ^ 1u);                  // :155-156
+                        last += last_slot ? (int)(inv_ps[r] >> 16) : 0;             // :93-96
+                    } else {
+                        h += (int)(((inv_poss[r] >> ro) & 1u) ^ 1u);
+                        last += last_slot ? inv_sn[r] : 0;
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            corr_words<0, EWC>(lds_addr(B), sv, inv_cup, lane, E, last_partial, h);   // :151-153
+            h = wave_sum(h);
+            last = wave_sum(last);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (lane == 0) {
+            if (any_bad) {
+                hcv_out[q] = -1; scv_io[q] = -1; feas_out[q] = 0; pen_out[q] = -1;
+            } else {
+                const int s2 = scv_io[q] + last;
+                hcv_out[q] = h;
+                scv_io[q] = s2;
+                feas_out[q] = h == 0 ? 1 : 0;
+                pen_out[q] = h == 0 ? s2 : 1000000 + h;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- eval_block
 constexpr int kBlockThreads = 256;
 
@@ -879,7 +1069,7 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
     if (P > 0 && (!hcv || !scv || !feasible || !penalty)) { set_error("null output buffer"); return TT_ERR_INVALID; }
     const int ablate = variant >> 4;   // profiling-only phase switches (tile kernel)
     variant &= 15;
-    if (variant < 0 || variant > 8) { set_error("unknown eval variant"); return TT_ERR_INVALID; }
+    if (variant < 0 || variant > 10) { set_error("unknown eval variant"); return TT_ERR_INVALID; }
     if (P == 0) return TT_OK;
     rc = use_device(p);
     if (rc) return rc;
@@ -937,6 +1127,46 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
             default: rc = TT_ERR_LIMIT; break;
         }
 #undef TT_T4
+        if (rc) return rc;
+    } else if (variant == 9 || variant == 10) {
+        // eval_lanes (8 or 4 waves per tile) then eval_waves, both on `st`
+        if (p->dev.EW64 > 7 || E > 32767) { set_error("instance too large for the split kernels"); return TT_ERR_LIMIT; }
+        const int NWL = variant == 9 ? 8 : 4;
+        int sp = (E + 1 + 3) & ~3;
+        if (((sp >> 2) & 1) == 0) sp += 4;
+        const size_t lds_l = (((size_t)64 * sp + 15) & ~(size_t)15) + 4 * (size_t)NWL * 64;
+        const int tiles = (P + 63) / 64;
+        auto launch_l = [&](auto kern) -> int {
+            int per_cu = 0;
+            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NWL, lds_l));
+            const int grid = std::min(tiles, std::max(1, per_cu) * p->num_cus);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NWL), lds_l, st, p->dev, slot, P, scv);
+            return TT_OK;
+        };
+        rc = NWL == 8 ? launch_l(eval_lanes_kernel<8>) : launch_l(eval_lanes_kernel<4>);
+        if (rc) return rc;
+        const int WS = tile5_layout(E, R, 8, false, false).WS;
+        const size_t lds_w = (size_t)kWavesWG * WS;
+        const int max_sn = p->student_number.empty() ? 0 : *std::max_element(p->student_number.begin(), p->student_number.end());
+        const int pk = (R <= 16 && max_sn <= 0xFFFF) ? 1 : R <= 32 ? 2 : 0;
+        auto launch_w = [&](auto kern) -> int {
+            int per_cu = 0;
+            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kWavesWG, lds_w));
+            const int grid = std::min((P + kWavesWG - 1) / kWavesWG, std::max(1, per_cu) * p->num_cus);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kWavesWG), lds_w, st, p->dev, slot, room, P, hcv, scv,
+                               feasible, penalty, WS);
+            return TT_OK;
+        };
+#define TT_TW(EWC)                                                                                  \
+    case EWC:                                                                                       \
+        rc = pk == 1 ? launch_w(eval_waves_kernel<EWC, 1>) : pk == 2 ? launch_w(eval_waves_kernel<EWC, 2>) \
+                     : launch_w(eval_waves_kernel<EWC, 0>);                                          \
+        break;
+        switch (p->dev.EW64) {
+            TT_TW(1) TT_TW(2) TT_TW(3) TT_TW(4) TT_TW(5) TT_TW(6) TT_TW(7)
+            default: rc = TT_ERR_LIMIT; break;
+        }
+#undef TT_TW
         if (rc) return rc;
     } else if (variant >= 5 && variant <= 8) {
         // 5/6: eval_tile5 with 4/8 waves, workspaces aliased on the tile, u32 cell
