@@ -124,3 +124,42 @@ def test_islands_cli_end_to_end(tmp_path, sm):
         rm = np.array(sol["rooms"], np.uint8)[None]
         h, sc, f, p = o.eval(s, rm)
         assert f[0] == 1 and sc[0] == sol["totalBest"] == runs[0]["totalBest"]
+
+
+def _json_lines(text):
+    """JSON lines with the wall-clock fields removed."""
+    out = []
+    for ln in text.splitlines():
+        if ln.startswith("{"):
+            obj = json.loads(ln)
+            for v in obj.values():
+                v.pop("time", None)
+                v.pop("totalTime", None)
+            out.append(obj)
+    return out
+
+
+def test_native_driver_matches_python_driver(tmp_path, sm):
+    """The C++ driver (ttga-ga, C-ABI + RCCL) and the Python driver
+    (ttga.islands) run the same GA on one GPU: identical JSON lines apart from
+    wall-clock times (log entries, run entries, the printed timetable)."""
+    inst, dp, o = sm
+    exe = REPO / "timetabling-ga-mpi-openmp_amd" / "ttga-ga"
+    assert exe.exists(), "ttga-ga not built (make -C timetabling-ga-mpi-openmp_amd)"
+    tim = tmp_path / "sm.tim"
+    ttga.write_tim(inst, tim)
+    args = ["-i", str(tim), "-s", "42", "-p", "1", "-c", "3", "--generations", "120", "--pop", "12"]
+    env = dict(__import__("os").environ, PYTHONPATH=str(REPO / "timetabling-ga-mpi-openmp_amd"))
+    py = subprocess.run([sys.executable, "-m", "ttga.islands", *args], capture_output=True, text=True, timeout=240,
+                        env=env, cwd=str(tmp_path))
+    cc = subprocess.run([str(exe), *args], capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    assert py.returncode == 0, py.stderr[-2000:]
+    assert cc.returncode == 0, cc.stderr[-2000:]
+    a, b = _json_lines(py.stdout), _json_lines(cc.stdout)
+    assert len(a) > 3 and a == b
+    assert "Max number of threads 3" in cc.stdout
+    assert "Warning: No output file given, writing to stdout" in cc.stderr
+    sol = [x["solution"] for x in b if "solution" in x][0]
+    if sol["feasible"]:
+        h, sc, f, p = o.eval(np.array(sol["timeslots"], np.uint8)[None], np.array(sol["rooms"], np.uint8)[None])
+        assert f[0] == 1 and sc[0] == sol["totalBest"]

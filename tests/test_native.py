@@ -54,3 +54,16 @@ def test_too_many_rooms_is_a_limit_error():
     out = ctypes.c_void_p()
     rc = lib.tt_problem_create(2, 65, 0, 1, rs.ctypes.data, A.ctypes.data, None, None, 0, ctypes.byref(out))
     assert rc == native.TT_ERR_LIMIT
+
+
+def test_native_driver_cli_errors_without_device():
+    """ttga-ga parses its command line as Control::Control (Control.cpp:7-39)
+    before touching a device: odd argument counts and a missing -i exit 1."""
+    import subprocess
+    exe = REPO / "timetabling-ga-mpi-openmp_amd" / "ttga-ga"
+    assert exe.exists(), "ttga-ga not built (make -C timetabling-ga-mpi-openmp_amd)"
+    r = subprocess.run([str(exe), "-s"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "Parse error: Number of command line parameters incorrect" in r.stderr
+    r = subprocess.run([str(exe), "-s", "5", "-c", "4"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "Error: No input file given, exiting" in r.stderr
+    assert "Max number of threads 4" in r.stdout

@@ -1,0 +1,579 @@
+// ttga-ga: the reference's ga.cpp driver (ga.cpp:370-613) as a native host
+// program over the C-ABI of include/ttga.h. One island per GPU of this node;
+// the MPI island model becomes RCCL over xGMI (one host thread and one
+// communicator rank per GPU, ncclCommInitAll), the OpenMP threads of a rank
+// become C children bred per batched generation.
+//
+//   ttga-ga -i instance.tim [-o out] [-s seed] [-p type] [-c children]
+//           [-p1 x -p2 y -p3 z] [--gpus K] [--pop N] [--generations G]
+//
+// Reference correspondence:
+//  * CLI: `-key value` pairs and messages of Control::Control (Control.cpp:3-137);
+//    -n -t -m -l are parsed and echoed, then ignored, as in ga.cpp.
+//  * -p -> maxSteps 200 / 1000 / 2000 (ga.cpp:389-397).
+//  * island k runs with seed abs(seed + k*(seed/10)) (ga.cpp:412); all islands
+//    start from island 0's initial population (ga.cpp:429-444,463-464).
+//  * generation loop, migration before generations g with (g+1) % 100 == 50,
+//    best -> right neighbour's pop[N-1], 2nd best -> left neighbour's pop[N-2]
+//    (ga.cpp:479-540); MIN all-reduce of the best value (ga.cpp:234-257);
+//    JSON lines of endTry / setCurrentCost / runEntry (ga.cpp:169-228,602-609)
+//    in jsoncpp's compact format (sorted keys, doubles as %.17g).
+//  * same stream layout as ttga/ga.py (Island): member i of the initial
+//    population draws from Random(|s|+1+i), child slot c from Random(|s|+1+N+c).
+#include <rccl/rccl.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <condition_variable>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/ttga.h"
+
+namespace {
+
+[[noreturn]] void die(const std::string& msg) {
+    std::cerr << "ttga-ga: " << msg << std::endl;
+    std::exit(1);
+}
+
+void check_tt(int rc, const char* what) {
+    if (rc != TT_OK) die(std::string(what) + ": " + tt_last_error());
+}
+
+void check_hip(hipError_t e, const char* what) {
+    if (e != hipSuccess) die(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void check_nccl(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess) die(std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+// ---------------------------------------------------------------- Control
+const char* kUsage = " -i InputFile [-o OutputFile] [-n NumberOfTries] [-s RandomSeed] [-t TimeLimit] [-p ProblemType]";
+
+struct Control {
+    int threads = 1, tries = 10, problem_type = 1, max_steps = 100;
+    double time_limit = 90, ls_limit = 99999, p1 = 1.0, p2 = 1.0, p3 = 0.0;
+    long seed = 0;
+    std::string input, output;
+    int gpus = 1, pop = 10, generations = -1;
+};
+
+// Control::Control (Control.cpp:3-137) plus the --gpus/--pop/--generations extensions.
+Control parse_control(int argc, char** argv) {
+    std::vector<std::string> args(argv + 1, argv + argc);
+    Control c;
+    for (const char* k : {"--gpus", "--pop", "--generations", "--children"}) {
+        auto it = std::find(args.begin(), args.end(), k);
+        if (it != args.end()) {
+            if (it + 1 == args.end()) die(std::string("missing value for ") + k);
+            const int v = std::atoi((it + 1)->c_str());
+            if (!std::strcmp(k, "--gpus")) c.gpus = v;
+            else if (!std::strcmp(k, "--pop")) c.pop = v;
+            else if (!std::strcmp(k, "--generations")) c.generations = v;
+            else c.threads = v;
+            args.erase(it, it + 2);
+        }
+    }
+    if (args.empty() || args.size() % 2 != 0) {
+        std::cerr << "Parse error: Number of command line parameters incorrect\n";
+        std::cerr << "Usage:" << std::endl << argv[0] << kUsage << std::endl;
+        std::exit(1);
+    }
+    std::map<std::string, std::string> kv;
+    for (size_t i = 0; i + 1 < args.size(); i += 2) kv[args[i]] = args[i + 1];
+    auto has = [&](const char* k) { return kv.count(k) > 0; };
+    if (has("-c")) {
+        c.threads = std::atoi(kv["-c"].c_str());
+        std::cout << "Max number of threads " << c.threads << std::endl;
+    } else {
+        std::cerr << "Warning: Number of threads is set to default (1)" << std::endl;
+    }
+    if (!has("-i")) {
+        std::cerr << "Error: No input file given, exiting" << std::endl;
+        std::cerr << "Usage:" << std::endl << argv[0] << kUsage << std::endl;
+        std::exit(1);
+    }
+    c.input = kv["-i"];
+    if (has("-o")) c.output = kv["-o"];
+    else std::cerr << "Warning: No output file given, writing to stdout" << std::endl;
+    if (has("-n")) {
+        c.tries = std::atoi(kv["-n"].c_str());
+        std::cout << "Max number of tries " << c.tries << std::endl;
+    } else {
+        std::cerr << "Warning: Number of tries is set to default (10)" << std::endl;
+    }
+    if (has("-t")) {
+        c.time_limit = std::atof(kv["-t"].c_str());
+        std::cout << "Time limit " << c.time_limit << std::endl;
+    } else {
+        std::cerr << "Warning: Time limit is set to default (90 sec)" << std::endl;
+    }
+    if (has("-p")) {
+        c.problem_type = std::atoi(kv["-p"].c_str());
+        std::cout << "Problem instance type " << c.problem_type << std::endl;
+    }
+    if (has("-m")) {
+        c.max_steps = std::atoi(kv["-m"].c_str());
+        std::cout << "Max number of steps in the local search " << c.max_steps << std::endl;
+    }
+    if (has("-l")) {
+        c.ls_limit = std::atof(kv["-l"].c_str());
+        std::cout << "Local search time limit " << c.ls_limit << std::endl;
+    } else {
+        std::cerr << "Warning: The local search time limit is set to default (99999 sec)" << std::endl;
+    }
+    struct P { const char* key; double* dst; const char* dflt; int n; };
+    for (P p : {P{"-p1", &c.p1, "1.0", 1}, P{"-p2", &c.p2, "1.0", 2}, P{"-p3", &c.p3, "0.0", 3}}) {
+        if (has(p.key)) {
+            *p.dst = std::atof(kv[p.key].c_str());
+            std::cout << "LS move " << p.n << " probability " << *p.dst << std::endl;
+        } else {
+            std::cerr << "Warning: The local search move " << p.n << " probability is set to default " << p.dflt
+                      << std::endl;
+        }
+    }
+    if (has("-s")) {
+        c.seed = std::atol(kv["-s"].c_str());
+    } else {
+        c.seed = (long)std::time(nullptr);
+        std::cerr << "Warning: " << c.seed << " used as default random seed" << std::endl;
+    }
+    return c;
+}
+
+// ga.cpp:389-397
+int max_steps_for(int problem_type) { return problem_type == 1 ? 200 : problem_type == 2 ? 1000 : 2000; }
+
+// ga.cpp:412 (C int division)
+long island_seed(long seed, int k) { return std::labs(seed + k * (seed / 10)); }
+
+// ---------------------------------------------------------------- .tim
+struct Instance {
+    int E = 0, R = 0, F = 0, S = 0;
+    std::vector<int32_t> room_size, student_events, room_features, event_features;
+};
+
+// Problem::Problem(istream&) token order (Problem.cpp:7-74).
+Instance read_tim(const std::string& path) {
+    std::ifstream in(path);
+    if (!in) die("cannot open " + path);
+    Instance t;
+    if (!(in >> t.E >> t.R >> t.F >> t.S)) die("truncated .tim header in " + path);
+    auto read = [&](std::vector<int32_t>& v, long n) {
+        v.resize(n);
+        for (long i = 0; i < n; i++)
+            if (!(in >> v[i])) die("truncated .tim body in " + path);
+    };
+    read(t.room_size, t.R);
+    read(t.student_events, (long)t.S * t.E);
+    read(t.room_features, (long)t.R * t.F);
+    read(t.event_features, (long)t.E * t.F);
+    return t;
+}
+
+// ---------------------------------------------------------------- JSON
+// jsoncpp StreamWriterBuilder with indentation "" (ga.cpp:170-171): compact,
+// keys in std::map order, doubles "%.17g" (jsoncpp.cpp:4036-4068).
+struct Json {
+    enum Kind { Int, Bool, Real, Arr, Obj } kind = Obj;
+    long i = 0;
+    double d = 0;
+    std::vector<long> arr;
+    std::map<std::string, Json> obj;
+    static Json I(long v) { Json j; j.kind = Int; j.i = v; return j; }
+    static Json B(bool v) { Json j; j.kind = Bool; j.i = v; return j; }
+    static Json D(double v) { Json j; j.kind = Real; j.d = v; return j; }
+    static Json A(std::vector<long> v) { Json j; j.kind = Arr; j.arr = std::move(v); return j; }
+    std::string str() const {
+        char buf[40];
+        switch (kind) {
+            case Int: return std::to_string(i);
+            case Bool: return i ? "true" : "false";
+            case Real:
+                if (std::isnan(d)) return "null";
+                if (std::isinf(d)) return d < 0 ? "-1e+9999" : "1e+9999";
+                std::snprintf(buf, sizeof buf, "%.17g", d);
+                return buf;
+            case Arr: {
+                std::string s = "[";
+                for (size_t k = 0; k < arr.size(); k++) s += (k ? "," : "") + std::to_string(arr[k]);
+                return s + "]";
+            }
+            case Obj: {
+                std::string s = "{";
+                bool first = true;
+                for (auto& kvp : obj) {
+                    s += (first ? "\"" : ",\"") + kvp.first + "\":" + kvp.second.str();
+                    first = false;
+                }
+                return s + "}";
+            }
+        }
+        return "";
+    }
+};
+
+Json wrap(const char* key, Json inner) {
+    Json j;
+    j.obj[key] = std::move(inner);
+    return j;
+}
+
+// ---------------------------------------------------------------- islands
+struct Pop {
+    int n = 0, E = 0;
+    uint8_t *slot = nullptr, *room = nullptr, *feasible = nullptr;
+    int32_t *hcv = nullptr, *scv = nullptr, *penalty = nullptr;
+    void alloc(int n_, int E_) {
+        n = n_; E = E_;
+        check_hip(hipMalloc(&slot, (size_t)n * E), "hipMalloc");
+        check_hip(hipMalloc(&room, (size_t)n * E), "hipMalloc");
+        check_hip(hipMalloc(&feasible, (size_t)n), "hipMalloc");
+        check_hip(hipMalloc(&hcv, 4 * (size_t)n), "hipMalloc");
+        check_hip(hipMalloc(&scv, 4 * (size_t)n), "hipMalloc");
+        check_hip(hipMalloc(&penalty, 4 * (size_t)n), "hipMalloc");
+        check_hip(hipMemset(slot, 0, (size_t)n * E), "hipMemset");
+        check_hip(hipMemset(room, 0, (size_t)n * E), "hipMemset");
+    }
+    void release() {
+        for (void* p : {(void*)slot, (void*)room, (void*)feasible, (void*)hcv, (void*)scv, (void*)penalty})
+            if (p) (void)hipFree(p);
+    }
+};
+
+struct Member { bool feasible; int scv, hcv, penalty; };
+
+class Output {
+public:
+    explicit Output(std::ostream& os) : os_(os) {}
+    void line(const Json& j) {
+        std::lock_guard<std::mutex> g(mu_);
+        os_ << j.str() << std::endl;
+    }
+private:
+    std::ostream& os_;
+    std::mutex mu_;
+};
+
+double seconds_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+struct Island {
+    int id = 0, device = 0, N = 0, C = 0, E = 0, max_steps = 0;
+    long seed = 0;
+    double p1 = 1, p2 = 1, p3 = 0, p_cross = 0.8, p_mut = 0.5;
+    tt_problem* tp = nullptr;
+    hipStream_t st = nullptr;
+    Pop pop, child;
+    int64_t *rng_init = nullptr, *rng_child = nullptr;
+    uint8_t* flags = nullptr;
+    void* work = nullptr;
+    uint8_t *send_buf = nullptr, *recv_buf = nullptr;   // one migrant: slot[E] room[E] hcv scv penalty feasible
+    size_t migrant_bytes = 0;
+    int best_scv = INT_MAX, best_eval = INT_MAX;      // setCurrentCost state (ga.cpp:163-167)
+
+    void setup(const Instance& inst) {
+        check_hip(hipSetDevice(device), "hipSetDevice");
+        check_tt(tt_problem_create(inst.E, inst.R, inst.F, inst.S, inst.room_size.data(), inst.student_events.data(),
+                                   inst.room_features.data(), inst.event_features.data(), device, &tp),
+                 "tt_problem_create");
+        E = inst.E;
+        check_hip(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+        pop.alloc(N, E);
+        child.alloc(C, E);
+        std::vector<int64_t> s(N + C);
+        for (int k = 0; k < N + C; k++) s[k] = std::labs(seed) + 1 + k;     // ttga/ga.py stream_seeds
+        check_hip(hipMalloc(&rng_init, 8 * (size_t)N), "hipMalloc");
+        check_hip(hipMalloc(&rng_child, 8 * (size_t)C), "hipMalloc");
+        check_hip(hipMemcpy(rng_init, s.data(), 8 * (size_t)N, hipMemcpyHostToDevice), "hipMemcpy");
+        check_hip(hipMemcpy(rng_child, s.data() + N, 8 * (size_t)C, hipMemcpyHostToDevice), "hipMemcpy");
+        check_hip(hipMalloc(&flags, (size_t)C), "hipMalloc");
+        check_hip(hipMalloc(&work, std::max<size_t>(tt_ga_work_bytes(N, E), 16)), "hipMalloc");
+        migrant_bytes = 2 * (size_t)E + 13;
+        check_hip(hipMalloc(&send_buf, migrant_bytes), "hipMalloc");
+        check_hip(hipMalloc(&recv_buf, migrant_bytes), "hipMalloc");
+    }
+
+    void evaluate(Pop& p) {
+        check_tt(tt_eval(tp, p.slot, p.room, p.n, p.hcv, p.scv, p.feasible, p.penalty, st), "tt_eval");
+    }
+
+    // ga.cpp:429-434 for every member, then the population is sorted
+    void initialize() {
+        check_tt(tt_random_init(tp, rng_init, pop.slot, pop.room, N, st), "tt_random_init");
+        check_tt(tt_local_search(tp, pop.slot, pop.room, rng_init, N, max_steps, p1, p2, p3, st), "tt_local_search");
+        evaluate(pop);
+        check_tt(tt_ga_replace(tp, pop.slot, pop.room, pop.hcv, pop.scv, pop.feasible, pop.penalty, N, pop.slot,
+                               pop.room, pop.hcv, pop.scv, pop.feasible, pop.penalty, 0, work, st),
+                 "tt_ga_replace");
+    }
+
+    // one generation of C children (ga.cpp:543-585)
+    void step() {
+        check_tt(tt_ga_breed(tp, pop.slot, pop.room, pop.penalty, N, rng_child, C, p_cross, p_mut, 1, child.slot,
+                             child.room, flags, st),
+                 "tt_ga_breed");
+        check_tt(tt_local_search(tp, child.slot, child.room, rng_child, C, max_steps, p1, p2, p3, st),
+                 "tt_local_search");
+        evaluate(child);
+        check_tt(tt_ga_replace(tp, pop.slot, pop.room, pop.hcv, pop.scv, pop.feasible, pop.penalty, N, child.slot,
+                               child.room, child.hcv, child.scv, child.feasible, child.penalty, C, work, st),
+                 "tt_ga_replace");
+    }
+
+    Member member(int k) {
+        Member m{};
+        uint8_t f = 0;
+        check_hip(hipMemcpyAsync(&f, pop.feasible + k, 1, hipMemcpyDeviceToHost, st), "hipMemcpy");
+        check_hip(hipMemcpyAsync(&m.scv, pop.scv + k, 4, hipMemcpyDeviceToHost, st), "hipMemcpy");
+        check_hip(hipMemcpyAsync(&m.hcv, pop.hcv + k, 4, hipMemcpyDeviceToHost, st), "hipMemcpy");
+        check_hip(hipMemcpyAsync(&m.penalty, pop.penalty + k, 4, hipMemcpyDeviceToHost, st), "hipMemcpy");
+        check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+        m.feasible = f != 0;
+        return m;
+    }
+
+    // setCurrentCost (ga.cpp:203-228) on pop[0]
+    void log_cost(Output& out, std::chrono::steady_clock::time_point t0) {
+        const Member m = member(0);
+        long entry = -1;
+        if (m.feasible) {
+            if (m.scv != best_scv) { best_scv = best_eval = m.scv; entry = m.scv; }
+        } else {
+            const long ev = (long)m.hcv * 1000000 + m.scv;
+            if (ev < best_eval) { best_eval = (int)ev; entry = ev; }
+        }
+        if (entry >= 0) {
+            Json e;
+            e.obj["best"] = Json::I(entry);
+            e.obj["procID"] = Json::I(id);
+            e.obj["threadID"] = Json::I(0);
+            e.obj["time"] = Json::D(std::max(0.0, seconds_since(t0)));
+            out.line(wrap("logEntry", e));
+        }
+    }
+
+    // serializeSolutions(k, 1, ...) (ga.cpp:318-342) into send_buf
+    void pack(int k) {
+        auto cp = [&](void* dst, const void* src, size_t n) {
+            check_hip(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+        };
+        cp(send_buf, pop.slot + (size_t)k * E, E);
+        cp(send_buf + E, pop.room + (size_t)k * E, E);
+        cp(send_buf + 2 * E, pop.hcv + k, 4);
+        cp(send_buf + 2 * E + 4, pop.scv + k, 4);
+        cp(send_buf + 2 * E + 8, pop.penalty + k, 4);
+        cp(send_buf + 2 * E + 12, pop.feasible + k, 1);
+    }
+
+    // deserializeSolution into position pos (ga.cpp:344-368)
+    void unpack(int pos, const uint8_t* buf) {
+        auto cp = [&](void* dst, const void* src, size_t n) {
+            check_hip(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+        };
+        cp(pop.slot + (size_t)pos * E, buf, E);
+        cp(pop.room + (size_t)pos * E, buf + E, E);
+        cp(pop.hcv + pos, buf + 2 * E, 4);
+        cp(pop.scv + pos, buf + 2 * E + 4, 4);
+        cp(pop.penalty + pos, buf + 2 * E + 8, 4);
+        cp(pop.feasible + pos, buf + 2 * E + 12, 1);
+    }
+
+    void release() {
+        pop.release();
+        child.release();
+        for (void* p : {(void*)rng_init, (void*)rng_child, (void*)flags, work, (void*)send_buf, (void*)recv_buf})
+            if (p) (void)hipFree(p);
+        if (st) (void)hipStreamDestroy(st);
+        if (tp) tt_problem_destroy(tp);
+    }
+};
+
+// Reusable barrier for the island threads (the MPI_Barrier calls of ga.cpp:520,538).
+class Barrier {
+public:
+    explicit Barrier(int n) : n_(n) {}
+    void wait() {
+        std::unique_lock<std::mutex> lk(mu_);
+        const long gen = gen_;
+        if (++count_ == n_) { count_ = 0; gen_++; cv_.notify_all(); return; }
+        cv_.wait(lk, [&] { return gen != gen_; });
+    }
+private:
+    std::mutex mu_;
+    std::condition_variable cv_;
+    int n_, count_ = 0;
+    long gen_ = 0;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const auto t0 = std::chrono::steady_clock::now();
+    Control ctl = parse_control(argc, argv);
+    std::ofstream file;
+    if (!ctl.output.empty()) {
+        file.open(ctl.output);
+        if (!file) die("cannot open " + ctl.output);
+    }
+    Output out(ctl.output.empty() ? std::cout : file);
+    const Instance inst = read_tim(ctl.input);
+
+    int ndev = 0;
+    check_hip(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    const int K = ctl.gpus;
+    if (K < 1 || K > ndev) die("--gpus " + std::to_string(K) + " but " + std::to_string(ndev) + " GPU(s) visible");
+    const int N = std::max(2, ctl.pop);
+    const int C = std::max(1, std::min(ctl.threads, N));
+    const int gens = ctl.generations >= 0 ? ctl.generations : (2001 + C - 1) / C;   // generations 0..2000 (ga.cpp:510)
+
+    std::vector<Island> isl(K);
+    for (int k = 0; k < K; k++) {
+        Island& I = isl[k];
+        I.id = k; I.device = k; I.N = N; I.C = C;
+        I.max_steps = max_steps_for(ctl.problem_type);
+        I.seed = island_seed(ctl.seed, k);
+        I.p1 = ctl.p1; I.p2 = ctl.p2; I.p3 = ctl.p3;
+    }
+    std::vector<ncclComm_t> comms(K, nullptr);
+    if (K > 1) {
+        std::vector<int> devs(K);
+        for (int k = 0; k < K; k++) devs[k] = k;
+        check_nccl(ncclCommInitAll(comms.data(), K, devs.data()), "ncclCommInitAll");
+    }
+    Barrier barrier(K);
+    std::vector<long> best_value(K, 0);
+    std::vector<int> best_feasible(K, 0);
+
+    auto run = [&](int k) {
+        Island& I = isl[k];
+        I.setup(inst);
+        if (k == 0) I.initialize();
+        if (K > 1) {   // every island starts from island 0's population (ga.cpp:442-464)
+            check_hip(hipStreamSynchronize(I.st), "hipStreamSynchronize");
+            barrier.wait();
+            check_nccl(ncclGroupStart(), "ncclGroupStart");
+            check_nccl(ncclBroadcast(I.pop.slot, I.pop.slot, (size_t)N * I.E, ncclUint8, 0, comms[k], I.st), "bcast");
+            check_nccl(ncclBroadcast(I.pop.room, I.pop.room, (size_t)N * I.E, ncclUint8, 0, comms[k], I.st), "bcast");
+            check_nccl(ncclBroadcast(I.pop.hcv, I.pop.hcv, N, ncclInt32, 0, comms[k], I.st), "bcast");
+            check_nccl(ncclBroadcast(I.pop.scv, I.pop.scv, N, ncclInt32, 0, comms[k], I.st), "bcast");
+            check_nccl(ncclBroadcast(I.pop.penalty, I.pop.penalty, N, ncclInt32, 0, comms[k], I.st), "bcast");
+            check_nccl(ncclBroadcast(I.pop.feasible, I.pop.feasible, N, ncclUint8, 0, comms[k], I.st), "bcast");
+            check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+        }
+        I.log_cost(out, t0);
+        const int right = (k + 1) % K, left = (k + K - 1) % K;
+        for (int g = 0; g < gens; g++) {
+            if ((g + 1) % 100 == 50) {   // ga.cpp:514-540, one migrant each way
+                check_hip(hipStreamSynchronize(I.st), "hipStreamSynchronize");
+                barrier.wait();
+                for (int dir = 0; dir < 2; dir++) {
+                    const int src_rank = std::min(dir, N - 1);      // best, then 2nd best
+                    const int pos = N - 1 - dir;                    // pop[N-1], then pop[N-2]
+                    I.pack(src_rank);
+                    if (K == 1) {
+                        I.unpack(pos, I.send_buf);
+                        continue;
+                    }
+                    const int to = dir == 0 ? right : left, from = dir == 0 ? left : right;
+                    check_nccl(ncclGroupStart(), "ncclGroupStart");
+                    check_nccl(ncclSend(I.send_buf, I.migrant_bytes, ncclUint8, to, comms[k], I.st), "ncclSend");
+                    check_nccl(ncclRecv(I.recv_buf, I.migrant_bytes, ncclUint8, from, comms[k], I.st), "ncclRecv");
+                    check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+                    I.unpack(pos, I.recv_buf);
+                }
+                check_hip(hipStreamSynchronize(I.st), "hipStreamSynchronize");
+                barrier.wait();
+            }
+            I.step();
+            I.log_cost(out, t0);
+        }
+        const Member b = I.member(0);
+        best_feasible[k] = b.feasible;
+        best_value[k] = b.feasible ? b.scv : (long)b.hcv * 1000000 + b.scv;
+    };
+    std::vector<std::thread> th;
+    for (int k = 0; k < K; k++) th.emplace_back(run, k);
+    for (auto& t : th) t.join();
+
+    // setGlobalCost (ga.cpp:234-257): MIN over islands through RCCL, printed by island 0
+    long gmin = best_value[0];
+    if (K > 1) {
+        std::vector<std::thread> red;
+        std::vector<int32_t*> dv(K, nullptr);
+        for (int k = 0; k < K; k++)
+            red.emplace_back([&, k] {
+                Island& I = isl[k];
+                check_hip(hipSetDevice(I.device), "hipSetDevice");
+                check_hip(hipMalloc(&dv[k], 8), "hipMalloc");
+                const int32_t v = (int32_t)best_value[k];
+                check_hip(hipMemcpy(dv[k], &v, 4, hipMemcpyHostToDevice), "hipMemcpy");
+                check_nccl(ncclAllReduce(dv[k], dv[k], 1, ncclInt32, ncclMin, comms[k], I.st), "ncclAllReduce");
+                check_hip(hipStreamSynchronize(I.st), "hipStreamSynchronize");
+            });
+        for (auto& t : red) t.join();
+        int32_t v = 0;
+        check_hip(hipSetDevice(0), "hipSetDevice");
+        check_hip(hipMemcpy(&v, dv[0], 4, hipMemcpyDeviceToHost), "hipMemcpy");
+        gmin = v;
+        for (int k = 0; k < K; k++) { (void)hipSetDevice(k); (void)hipFree(dv[k]); }
+    }
+    {
+        Json r;
+        r.obj["feasible"] = Json::B(best_feasible[0] != 0);
+        r.obj["totalBest"] = Json::I(gmin);
+        out.line(wrap("runEntry", r));
+    }
+    // endTry (ga.cpp:169-197) per island
+    for (int k = 0; k < K; k++) {
+        Island& I = isl[k];
+        check_hip(hipSetDevice(I.device), "hipSetDevice");
+        const Member b = I.member(0);
+        Json s;
+        s.obj["feasible"] = Json::B(b.feasible);
+        s.obj["procID"] = Json::I(k);
+        s.obj["threadID"] = Json::I(0);
+        s.obj["totalTime"] = Json::D(seconds_since(t0));
+        if (b.feasible) {
+            s.obj["totalBest"] = Json::I(b.scv);
+            std::vector<uint8_t> sl(I.E), rm(I.E);
+            check_hip(hipMemcpy(sl.data(), I.pop.slot, I.E, hipMemcpyDeviceToHost), "hipMemcpy");
+            check_hip(hipMemcpy(rm.data(), I.pop.room, I.E, hipMemcpyDeviceToHost), "hipMemcpy");
+            s.obj["timeslots"] = Json::A(std::vector<long>(sl.begin(), sl.end()));
+            s.obj["rooms"] = Json::A(std::vector<long>(rm.begin(), rm.end()));
+        } else {
+            s.obj["totalBest"] = Json::I((long)b.hcv * 1000000 + b.scv);
+        }
+        out.line(wrap("solution", s));
+    }
+    {
+        Json r;
+        r.obj["procsNum"] = Json::I(K);
+        r.obj["threadsNum"] = Json::I(C);
+        r.obj["totalTime"] = Json::D(seconds_since(t0));
+        out.line(wrap("runEntry", r));
+    }
+    for (int k = 0; k < K; k++) {
+        (void)hipSetDevice(isl[k].device);
+        isl[k].release();
+        if (comms[k]) ncclCommDestroy(comms[k]);
+    }
+    return 0;
+}
