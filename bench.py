@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--pop", type=int, default=POP_PER_GPU)
     ap.add_argument("--config", default="med", choices=["sm", "med", "lg", "syn"])
     ap.add_argument("--variant", type=int, default=0, help="tt_eval kernel: 0 auto, 1 lanes, 2 block")
-    ap.add_argument("--cpu-sample", type=int, default=16384, help="individuals in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=65536, help="individuals in the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
