@@ -240,4 +240,66 @@ void ref_mutation(void* p, u8* slot, u8* room, long* rng, int np) {
     }
 }
 
+// The per-child work of the reference's generation loop (ga.cpp:543-577),
+// OpenMP over children, each child with its own Random: three
+// RandomInitialSolution (child, copyParent1, copyParent2), two selection5
+// tournaments over pop_penalty (restated from ga.cpp:129-145: first drawn wins
+// ties), the parent copies, next() < 0.8 ? crossover : copy, next() < 0.5 ?
+// mutation, localSearch(max_steps), computePenalty. as_is = 1: as in the
+// reference, the crossover child is the one that already holds a random
+// solution (F2: its timeslot lists then hold every event twice, which slows
+// the matching and the local search); as_is = 0: crossover into a fresh
+// Solution, the semantics the device engine implements.
+// Only the time is of interest (bench CPU baseline). Returns seconds.
+double ref_ga_children_timed(void* p, const u8* pop_slot, const u8* pop_room, const int* pop_penalty, int N,
+                             long* rng, int C, int max_steps, int threads, int as_is) {
+    Problem* P = (Problem*)p;
+    const int E = P->n_of_events;
+    omp_set_num_threads(threads);
+    struct timeval t0, t1;
+    gettimeofday(&t0, 0);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int c = 0; c < C; c++) {
+        Random r(0);
+        r.seed = rng[c];
+        Solution* child = new Solution(P, &r);
+        child->RandomInitialSolution();
+        Solution* cp1 = new Solution(P, &r);
+        cp1->RandomInitialSolution();
+        Solution* cp2 = new Solution(P, &r);
+        cp2->RandomInitialSolution();
+        int sel[2];
+        for (int k = 0; k < 2; k++) {
+            int best = (int)(r.next() * N);
+            for (int i = 1; i < 5; i++) {
+                const int t = (int)(r.next() * N);
+                if (pop_penalty[t] < pop_penalty[best]) best = t;
+            }
+            sel[k] = best;
+        }
+        Solution a(P, &r), b(P, &r);
+        load_solution(&a, pop_slot + (long)sel[0] * E, pop_room + (long)sel[0] * E, E);
+        load_solution(&b, pop_slot + (long)sel[1] * E, pop_room + (long)sel[1] * E, E);
+        cp1->copy(&a);
+        cp2->copy(&b);
+        Solution* use = child;
+        Solution fresh(P, &r);
+        if (r.next() < 0.8) {
+            if (as_is) child->crossover(cp1, cp2);
+            else { fresh.crossover(cp1, cp2); use = &fresh; }
+        } else {
+            use = cp1;
+        }
+        if (r.next() < 0.5) use->mutation();
+        use->localSearch(max_steps);
+        use->computePenalty();
+        rng[c] = r.seed;
+        delete child;
+        delete cp1;
+        delete cp2;
+    }
+    gettimeofday(&t1, 0);
+    return (t1.tv_sec - t0.tv_sec) + 1e-6 * (t1.tv_usec - t0.tv_usec);
+}
+
 }  // extern "C"

@@ -126,6 +126,23 @@ def generate(E: int, R: int, F: int, S: int, seed: int = 1, min_att: int = 5, ma
     return Instance(E, R, F, S, sizes, A, rf, ef)
 
 
+def comp_dims(k: int) -> tuple[int, int, int, int]:
+    """(E, R, F, S) of the ITC-2002-like instance compK (k = 1..20): E in
+    [350, 440], R in {10, 11}, F = 10, S in [200, 350], drawn from
+    Park-Miller seeded with 7919 * k."""
+    rng = ParkMiller(7919 * int(k))
+    E = 350 + int(rng.next() * 91)
+    R = 10 + int(rng.next() * 2)
+    S = 200 + int(rng.next() * 151)
+    return E, R, 10, S
+
+
 def config_instance(name: str, seed: int = 1) -> Instance:
+    """sm / med / lg / syn (CONFIGS) or comp01 .. comp20 (seed k)."""
+    if name.startswith("comp"):
+        k = int(name[4:])
+        if not 1 <= k <= 20:
+            raise ValueError("comp instances are comp01 .. comp20")
+        return generate(*comp_dims(k), seed=k)
     E, R, F, S = CONFIGS[name]
     return generate(E, R, F, S, seed=seed)

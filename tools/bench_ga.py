@@ -1,0 +1,98 @@
+"""Full-GA throughput (BASELINE configs[2]: ITC-2002-like comp instances,
+population 65,536, full GA on one MI355X vs the host-CPU reference).
+
+GPU: one island (ttga.ga.Island) with N members and C children per generation;
+a generation is breed (selection5 x2, crossover p 0.8 / copy, mutation p 0.5)
++ localSearch(maxSteps) + evaluation + replace-worst + sort, all batched on the
+device. Metric: children per second over G timed generations (after the
+initial population is built and one warm-up generation).
+
+CPU: the reference's own per-child path of ga.cpp:543-577 (three
+RandomInitialSolution, two selection5, copies, crossover/copy, mutation,
+localSearch, computePenalty) on the host cores, OpenMP over children
+(oracle/_ref ref_ga_children_timed), on a sample of children bred from the
+same population. The reference's replace-worst + sort of its 10-member
+population is omitted from its timing (negligible there).
+
+    python tools/bench_ga.py [--config comp01] [--pop 65536] [--children 65536]
+                             [--gens 3] [--steps 200] [--cpu-sample 512]
+"""
+import argparse
+import ctypes
+import json
+import os
+import pathlib
+import sys
+import time
+
+REPO = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "timetabling-ga-mpi-openmp_amd"))
+sys.path.insert(0, str(REPO / "tests"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import ttga  # noqa: E402
+from ttga import native  # noqa: E402
+from ttga.ga import Island  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="comp01")
+ap.add_argument("--pop", type=int, default=65536)
+ap.add_argument("--children", type=int, default=65536)
+ap.add_argument("--gens", type=int, default=3)
+ap.add_argument("--steps", type=int, default=200, help="maxSteps (-p 1: 200, -p 2: 1000, else 2000)")
+ap.add_argument("--seed", type=int, default=42)
+ap.add_argument("--cpu-sample", type=int, default=512)
+a = ap.parse_args()
+
+inst = ttga.config_instance(a.config)
+dp = native.DeviceProblem(inst)
+isl = Island(dp, pop_size=a.pop, children=a.children, max_steps=a.steps, seed=a.seed)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+isl.initialize()
+torch.cuda.synchronize()
+init_s = time.perf_counter() - t0
+isl.step()                                  # warm-up generation
+torch.cuda.synchronize()
+# snapshot of the population the CPU sample breeds from
+pop_slot, pop_room = isl.pop["slot"].cpu().numpy().copy(), isl.pop["room"].cpu().numpy().copy()
+pop_pen = isl.pop["penalty"].cpu().numpy().copy()
+t0 = time.perf_counter()
+for _ in range(a.gens):
+    isl.step()
+torch.cuda.synchronize()
+gpu_s = time.perf_counter() - t0
+feas, scv, hcv, pen = isl.member_meta(0)
+out = {"config": a.config, "E": inst.E, "R": inst.R, "F": inst.F, "S": inst.S, "pop": a.pop,
+       "children_per_gen": a.children, "gens": a.gens, "max_steps": a.steps, "init_seconds": init_s,
+       "gpu_seconds": gpu_s, "gpu_children_per_s": a.children * a.gens / gpu_s,
+       "best": {"feasible": feas, "scv": scv, "hcv": hcv, "penalty": pen},
+       "feasible_fraction": float(isl.pop["feasible"].float().mean().item())}
+
+from oracle_lib import ref  # noqa: E402
+R = ref()
+if R is not None and a.cpu_sample > 0:
+    n = a.cpu_sample
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    fn = R.lib.ref_ga_children_timed
+    fn.restype = ctypes.c_double
+    fn.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_void_p] + [ctypes.c_int] * 4
+    h = R.problem(inst)
+    P_ = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    pen32 = np.ascontiguousarray(pop_pen, dtype=np.int32)
+    res = {}
+    for as_is in (0, 1):
+        rng = ttga.population_seeds(777, n)
+        res[as_is] = fn(h.h, P_(pop_slot), P_(pop_room), P_(pen32), a.pop, P_(rng), n, a.steps, threads, as_is)
+    out["cpu_baseline"] = {"kind": "reference", "cores": threads, "sample_children": n, "seconds": res[0],
+                           "children_per_s": n / res[0],
+                           "what": "ga.cpp:543-577 per child (3x RandomInitialSolution, 2x selection5, copies, "
+                                   "crossover into a fresh child / copy, mutation, localSearch, computePenalty), "
+                                   "OpenMP over children",
+                           "as_is_children_per_s": n / res[1],
+                           "as_is_note": "crossover into the child that already holds a random solution, as "
+                                         "ga.cpp:543-563 does (SURVEY F2); its doubled slot lists change the "
+                                         "local search's work; context only, not used for the speedup"}
+    out["speedup_vs_cpu"] = out["gpu_children_per_s"] / out["cpu_baseline"]["children_per_s"]
+print(json.dumps(out))
