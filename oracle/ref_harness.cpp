@@ -11,6 +11,7 @@
 // -ftrivial-auto-var-init=zero, which zero-fills that VLA.
 //
 // Written in C++98 (the reference's Random.h needs gnu++98).
+#include <algorithm>
 #include <sstream>
 #include <vector>
 #include <sys/time.h>
@@ -297,6 +298,100 @@ double ref_ga_children_timed(void* p, const u8* pop_slot, const u8* pop_room, co
         delete child;
         delete cp1;
         delete cp2;
+    }
+    gettimeofday(&t1, 0);
+    return (t1.tv_sec - t0.tv_sec) + 1e-6 * (t1.tv_usec - t0.tv_usec);
+}
+
+static bool by_penalty(Solution* a, Solution* b) { return a->penalty < b->penalty; }   // ga.cpp:150-153
+
+// The value setCurrentCost logs for pop[0] (ga.cpp:203-228): scv if feasible,
+// else computeHcv()*1e6 + computeScv() (which also refreshes both fields).
+static long log_value(Solution* s) {
+    if (s->feasible) return s->scv;
+    const long h = s->computeHcv();
+    return h * 1000000L + s->computeScv();
+}
+
+// Whole single-island GA runs of the reference, one per seed, for the
+// statistical comparison of GA trajectories (tools/ga_quality.py). Each run is
+// ga.cpp with one MPI rank and one OpenMP thread (-c 1), restated around the
+// reference's own Solution objects: Random(seed) (ga.cpp:400-401); pop_size
+// members RandomInitialSolution + localSearch(max_steps) + computePenalty
+// (:429-434); then generations 0..gens-1 (ga.cpp runs gens = 2001,
+// :504), each: three RandomInitialSolution, two selection5 (:129-145),
+// next() < 0.8 ? crossover : copy of parent 1, next() < 0.5 ? mutation,
+// localSearch, computePenalty, pop[N-1]->copy(child), std::sort (:543-585).
+// as_is = 1 keeps F2 (crossover into the child that already holds a random
+// solution, as ga.cpp:543-563); as_is = 0 crosses into a fresh Solution.
+// No migration (one island). Runs are independent: OpenMP over seeds.
+// Outputs per run: best hcv, scv, feasible, penalty after the last
+// generation (hcv recomputed, as endTry does, ga.cpp:189), and trace[run][g] =
+// the value setCurrentCost logs for pop[0] after generation g (g = 0: the
+// sorted initial population).
+double ref_ga_run(void* p, const long* seeds, int runs, int pop_size, int gens, int max_steps, int as_is,
+                  int threads, int* hcv, int* scv, u8* feasible, int* penalty, long* trace) {
+    Problem* P = (Problem*)p;
+    omp_set_num_threads(threads);
+    struct timeval t0, t1;
+    gettimeofday(&t0, 0);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int k = 0; k < runs; k++) {
+        Random rnd(seeds[k]);
+        std::vector<Solution*> pop(pop_size);
+        for (int i = 0; i < pop_size; i++) {
+            pop[i] = new Solution(P, &rnd);
+            pop[i]->RandomInitialSolution();
+            pop[i]->localSearch(max_steps);
+            pop[i]->computePenalty();
+        }
+        std::sort(pop.begin(), pop.end(), by_penalty);
+        long* tr = trace ? trace + (long)k * (gens + 1) : 0;
+        const long v0 = log_value(pop[0]);
+        if (tr) tr[0] = v0;
+        for (int g = 0; g < gens; g++) {
+            Solution* child = new Solution(P, &rnd);
+            child->RandomInitialSolution();
+            Solution* cp1 = new Solution(P, &rnd);
+            cp1->RandomInitialSolution();
+            Solution* cp2 = new Solution(P, &rnd);
+            cp2->RandomInitialSolution();
+            Solution* sel[2];
+            for (int s = 0; s < 2; s++) {
+                int best = (int)(rnd.next() * pop_size);
+                for (int i = 1; i < 5; i++) {
+                    const int t = (int)(rnd.next() * pop_size);
+                    if (pop[t]->penalty < pop[best]->penalty) best = t;
+                }
+                sel[s] = pop[best];
+            }
+            cp1->copy(sel[0]);
+            cp2->copy(sel[1]);
+            Solution* use = child;
+            Solution* fresh = 0;
+            if (rnd.next() < 0.8) {
+                if (as_is) child->crossover(cp1, cp2);
+                else { fresh = new Solution(P, &rnd); fresh->crossover(cp1, cp2); use = fresh; }
+            } else {
+                use = cp1;
+            }
+            if (rnd.next() < 0.5) use->mutation();
+            use->localSearch(max_steps);
+            use->computePenalty();
+            pop[pop_size - 1]->copy(use);
+            std::sort(pop.begin(), pop.end(), by_penalty);
+            const long v = log_value(pop[0]);
+            if (tr) tr[g + 1] = v;
+            delete child;
+            delete cp1;
+            delete cp2;
+            delete fresh;
+        }
+        hcv[k] = pop[0]->computeHcv();
+        scv[k] = pop[0]->computeScv();
+        feasible[k] = pop[0]->feasible ? 1 : 0;
+        penalty[k] = pop[0]->penalty;
+        for (int i = 0; i < pop_size; i++) delete pop[i];
     }
     gettimeofday(&t1, 0);
     return (t1.tv_sec - t0.tv_sec) + 1e-6 * (t1.tv_usec - t0.tv_usec);

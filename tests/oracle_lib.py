@@ -169,3 +169,22 @@ def oracle():
 def ref():
     """The reference build, or None where it was never built (no /root/reference)."""
     return Ref(REF_PATH) if REF_PATH.exists() else None
+
+
+def _ga_run(self, seeds, pop_size=10, gens=2001, max_steps=200, as_is=1, threads=1):
+    """ref_ga_run: whole single-island reference GA runs, one per seed (Ref only).
+    Returns (hcv, scv, feasible, penalty, trace[runs, gens+1], seconds)."""
+    seeds = np.ascontiguousarray(seeds, np.int64)
+    n = seeds.size
+    hcv = np.zeros(n, np.int32); scv = np.zeros(n, np.int32)
+    feas = np.zeros(n, np.uint8); pen = np.zeros(n, np.int32)
+    trace = np.zeros((n, gens + 1), np.int64)
+    fn = self.c._f("ga_run")
+    fn.restype = ctypes.c_double
+    fn.argtypes = [_vp, _vp] + [ctypes.c_int] * 6 + [_vp] * 5
+    secs = fn(self.h, _p(seeds), n, int(pop_size), int(gens), int(max_steps), int(as_is), int(threads),
+              _p(hcv), _p(scv), _p(feas), _p(pen), _p(trace))
+    return hcv, scv, feas, pen, trace, secs
+
+
+_Handle.ga_run = _ga_run

@@ -163,3 +163,30 @@ def test_native_driver_matches_python_driver(tmp_path, sm):
     if sol["feasible"]:
         h, sc, f, p = o.eval(np.array(sol["timeslots"], np.uint8)[None], np.array(sol["rooms"], np.uint8)[None])
         assert f[0] == 1 and sc[0] == sol["totalBest"]
+
+
+def test_ga_trajectories_match_reference_statistically(sm):
+    """Whole-GA outcomes over fixed seeds (the RNG streams differ):
+    the device GA (pop 10, one child per generation) against the reference's
+    own ga.cpp loop (oracle/_ref ref_ga_run, fresh crossover child) on the sm
+    instance, 1000 generations, maxSteps 200. Same feasibility rate (Fisher)
+    and no detectable shift of the final best (Mann-Whitney U, p > 0.01).
+    tools/ga_quality.py is the full 16-seed x 2001-generation version
+    (profiles/r01_ga_quality_sm.json)."""
+    from oracle_lib import ref
+    R = ref()
+    if R is None:
+        pytest.skip("reference build oracle/_ref not present")
+    stats = pytest.importorskip("scipy.stats")
+    sys.path.insert(0, str(REPO / "tools"))
+    from ga_quality import device_runs
+    inst = sm[0]
+    seeds, gens = list(range(1, 9)), 1000
+    _, _, rfeas, _, rtrace, _ = R.problem(inst).ga_run(seeds, 10, gens, 200, 0, 8)
+    dfinal, dfeas, dtrace, _ = device_runs(inst, seeds, 10, gens, 200)
+    # the logged best never gets worse along a trajectory (ga.cpp keeps pop[0])
+    assert np.all(np.diff(dtrace, axis=1) <= 0)
+    table = [[int(dfeas.sum()), int(len(seeds) - dfeas.sum())], [int(rfeas.sum()), int(len(seeds) - rfeas.sum())]]
+    assert stats.fisher_exact(table)[1] > 0.01
+    p = stats.mannwhitneyu(dfinal, rtrace[:, -1], alternative="two-sided").pvalue
+    assert p > 0.01, (dfinal, rtrace[:, -1], p)

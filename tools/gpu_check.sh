@@ -27,6 +27,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py ;;
     phases) run phases 300 python -u tools/prof_eval.py med 65536 ;;
+    quality) run ga_quality 900 python -u tools/ga_quality.py --config sm --seeds 16 --gens 2001 --steps 200 --out "$OUT/ga_quality_sm.json" ;;
     ls)    run bench_ls 600 python -u tools/bench_ls.py --pop 4096 --steps 200 ;;
     ls1000) run bench_ls1000 600 python -u tools/bench_ls.py --pop 4096 --steps 1000 --cpu-sample 256 ;;
     listpmc) run listpmc 120 rocprofv3 -L ;;
