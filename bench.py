@@ -30,8 +30,11 @@ sys.path.insert(0, str(REPO / "tests"))
 METRIC = json.loads((REPO / "BASELINE.json").read_text())["metric"]
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 POP_PER_GPU = 65536
+SIZE_NAMES = {"sm": "small01-size", "med": "medium01-size", "lg": "large01-size",
+              "syn": "synthetic 2000/40/10/5000 scaling instance"}
 KERNELS = {1: "eval_tile", 2: "eval_block", 3: "eval_tile4", 4: "eval_tile4_w8", 5: "eval_tile5_alias",
-           6: "eval_tile5_alias_w8", 7: "eval_tile5", 8: "eval_tile5_w8"}
+           6: "eval_tile5_alias_w8", 7: "eval_tile5", 8: "eval_tile5_w8",
+           9: "eval_lanes_w8+eval_waves", 10: "eval_lanes+eval_waves"}
 
 
 def parse():
@@ -42,7 +45,9 @@ def parse():
     ap.add_argument("--pop", type=int, default=POP_PER_GPU)
     ap.add_argument("--config", default="med", choices=["sm", "med", "lg", "syn"])
     ap.add_argument("--variant", type=int, default=0, help="tt_eval kernel: 0 auto, 1 lanes, 2 block")
-    ap.add_argument("--cpu-sample", type=int, default=65536, help="individuals in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="individuals in the CPU-baseline sample (0: sized to about --cpu-seconds of CPU work)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
@@ -154,7 +159,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": wall_max / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "i32", "data": "synthetic",
             "config": {"workload": f"{args.config} instance E={E} R={inst.R} F={inst.F} S={inst.S} (seeded synthetic, "
-                                   f"medium01-size), population {P} per GPU, one tt_eval (hcv+scv+feasible+penalty) "
+                                   f"{SIZE_NAMES[args.config]}), population {P} per GPU, one tt_eval (hcv+scv+feasible+penalty) "
                                    f"per step", "pop_per_gpu": P, "global_pop": P * world,
                        "kernel": KERNELS[variant],
                        "parallelism": f"dp{world} (independent population shards)"},
@@ -163,7 +168,13 @@ def main():
                          "kernel_ms": kernel_ms, "bytes_per_eval": bytes_per_eval},
         }
         if world == 1 and not args.no_cpu:
-            n = min(args.cpu_sample, P)
+            n = args.cpu_sample
+            if n <= 0:      # calibrate on a small slice, then size the sample to ~cpu_seconds
+                n0 = min(P, 256)
+                c = cpu_baseline(inst, slot[:n0].cpu().numpy(), room[:n0].cpu().numpy(),
+                                 [o[:n0].cpu().numpy() for o in out])
+                n = int(max(n0, min(P, c["value"] * args.cpu_seconds)))
+            n = min(n, P)
             s_np, r_np = slot[:n].cpu().numpy(), room[:n].cpu().numpy()
             gpu_out = [o[:n].cpu().numpy() for o in out]
             line["cpu_baseline"] = cpu_baseline(inst, s_np, r_np, gpu_out)

@@ -26,6 +26,8 @@ for s in $STEPS; do
     gatests) run pytest_ga 600 python -u -m pytest tests/test_gpu_ga.py -m gpu -v --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py ;;
+    benchsyn) run bench_syn 600 python -u bench.py --config syn --pop 262144 --steps 10 --warmup 2 ;;
+    benchlg) run bench_lg 600 python -u bench.py --config lg --steps 100 ;;
     phases) run phases 300 python -u tools/prof_eval.py med 65536 ;;
     quality) run ga_quality 900 python -u tools/ga_quality.py --config sm --seeds 16 --gens 2001 --steps 200 --out "$OUT/ga_quality_sm.json" ;;
     ls)    run bench_ls 600 python -u tools/bench_ls.py --pop 4096 --steps 200 ;;
