@@ -34,7 +34,7 @@ SIZE_NAMES = {"sm": "small01-size", "med": "medium01-size", "lg": "large01-size"
               "syn": "synthetic 2000/40/10/5000 scaling instance"}
 KERNELS = {1: "eval_tile", 2: "eval_block", 3: "eval_tile4", 4: "eval_tile4_w8", 5: "eval_tile5_alias",
            6: "eval_tile5_alias_w8", 7: "eval_tile5", 8: "eval_tile5_w8",
-           9: "eval_lanes_w8+eval_waves", 10: "eval_lanes+eval_waves"}
+           9: "eval_lanes_w8+eval_waves", 10: "eval_lanes+eval_waves", 13: "eval_lanes_w16+eval_wide"}
 
 
 def parse():

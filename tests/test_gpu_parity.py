@@ -13,8 +13,9 @@ torch = pytest.importorskip("torch")
 from ttga import native  # noqa: E402
 
 NAMES = ["sm", "med", "tight"]
-# tt_eval kernels: 1 eval_tile, 2 eval_block, 3/4 eval_tile4 (4/8 waves), 5-8 eval_tile5, 9/10 split
-EVAL_VARIANTS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10]
+# tt_eval kernels: 1 eval_tile, 2 eval_block, 3/4 eval_tile4 (4/8 waves), 5-8 eval_tile5, 9/10 split,
+# 13 wide path (eval_lanes<16> + eval_wide)
+EVAL_VARIANTS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13]
 
 
 def load(golden_dir, name):
@@ -87,6 +88,32 @@ def test_eval_random_vs_oracle(orc, variant, dims):
     exp = orc.problem(inst).eval(slots, rooms)
     for g, e in zip(got, exp):
         assert np.array_equal(g, e)
+
+
+@pytest.mark.parametrize("dims", [(1000, 20, 6, 700), (1531, 64, 8, 900), (2430, 33, 5, 600), (449, 10, 5, 200)],
+                         ids=["E1000R20", "E1531R64", "E2430R33", "E449R10"])
+def test_eval_wide_vs_oracle(orc, dims):
+    """Instances beyond eval_tile5 (E > 448): the wide path (variant 13, the
+    automatic choice there) and the workgroup kernel against the oracle; E not a
+    multiple of 4 (byte row loads), R = 64 (full room masks), the largest E the
+    wide path takes, and the first E past eval_tile5."""
+    inst = ttga.generate(*dims, seed=13)
+    dp = native.DeviceProblem(inst)
+    assert dp.eval_variant() == 13
+    P = 133
+    slots, _ = ttga.random_slots(ttga.population_seeds(777, P), inst.E)
+    rng = np.random.default_rng(9)
+    rooms = rng.integers(0, inst.R, size=(P, inst.E), dtype=np.uint8)
+    rooms[::2] = orc.problem(inst).assign_rooms(slots[::2])
+    exp = orc.problem(inst).eval(slots, rooms)
+    slots[5, inst.E - 1] = 45                          # invalid gene in the last (partial) chunk: sentinels
+    exp[0][5] = exp[1][5] = exp[3][5] = -1
+    exp[2][5] = 0
+    variants = [2, 13] + ([1] if inst.E <= 1024 else [])
+    for v in variants:
+        got = [host(t) for t in dp.eval(dev(slots), dev(rooms), variant=v)]
+        for g, e in zip(got, exp):
+            assert np.array_equal(g, e), v
 
 
 def test_eval_invalid_individual_flagged(problems):
@@ -170,14 +197,18 @@ def test_random_init_crossover_mutation_golden(problems, name):
 
 
 def test_syn_scale_instance(orc):
-    """Synthetic 2000/40/10/5000 instance (BASELINE configs[4]): the lane kernel
-    is out of range so tt_eval uses the workgroup kernel; spot-check vs oracle."""
+    """Synthetic 2000/40/10/5000 instance (BASELINE configs[4]): tt_eval takes the
+    wide path; it agrees with the workgroup kernel on every individual and with
+    the oracle on a sample."""
     inst = ttga.config_instance("syn")
     dp = native.DeviceProblem(inst)
+    assert dp.eval_variant() == 13
     P = 512
     slots, _ = ttga.random_slots(ttga.population_seeds(31, P), inst.E)
     room = dp.assign_rooms(dev(slots))
     hcv, scv, feas, pen = (host(t) for t in dp.eval(dev(slots), room))
+    for x, y in zip((hcv, scv, feas, pen), (host(t) for t in dp.eval(dev(slots), room, variant=2))):
+        assert np.array_equal(x, y)
     idx = np.array([0, 1, 255, 511])
     o = orc.problem(inst)
     r_np = host(room)[idx]

@@ -40,10 +40,12 @@ struct DevProblem {
     const int32_t* stc_ev;        //   padding entries hold E (a sentinel column)
     const uint4* sch;             // the same records in student order (eval_tile4)
     const int32_t* sch_part;      // record offsets of each wave's contiguous student range:
-                                  //   [kSchPart4 + w] for 4-wave, [kSchPart8 + w] for 8-wave groups
+                                  //   [kSchPart4 + w] for 4-wave, [kSchPart8 + w] for 8-wave and
+                                  //   [kSchPart16 + w] for 16-wave groups
     int32_t* status;              // device status word (tt_device_status)
 };
-constexpr int kSchPart4 = 0, kSchPart8 = 5, kSchPartLen = 16;
+constexpr int kSchPart4 = 0, kSchPart8 = 5, kSchPart16 = 14, kSchPartLen = 32;
+__host__ __device__ constexpr int sch_part_base(int nw) { return nw == 4 ? kSchPart4 : nw == 8 ? kSchPart8 : kSchPart16; }
 
 // Park-Miller "minimal standard" generator, Schrage's method
 // (Random.h:15-19, Random.cc:27-37). Bit-exact with the reference: int64

@@ -790,11 +790,11 @@ __global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, con
     const int tiles = (P + 63) / 64;
     const ConstU32* rec = (const ConstU32*)pb.sch;
     const ConstI32* ptab = (const ConstI32*)pb.sch_part;
-    const int pbase = NWL == 4 ? kSchPart4 : kSchPart8;
+    const int pbase = sch_part_base(NWL);
     const int c0 = ptab[pbase + wv], c1 = ptab[pbase + wv + 1];
     const bool wide = (E & 15) == 0 && (((uintptr_t)slot) & 15) == 0;
     const int qpr = E >> 4;
-    const uint32_t qinv = ((1u << 20) + (uint32_t)qpr - 1) / (uint32_t)max(qpr, 1);
+    const uint64_t qinv = ((1ull << 32) + (uint64_t)qpr - 1) / (uint64_t)max(qpr, 1);   // exact w / qpr below
 
     for (int tl = blockIdx.x; tl < tiles; tl += gridDim.x) {
         const long p0 = (long)tl * 64;
@@ -805,7 +805,7 @@ __global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, con
             const uint4* s16 = (const uint4*)src;
 #pragma unroll 2
             for (int w = threadIdx.x; w < np * qpr; w += NT) {
-                const int r = (int)(((uint32_t)w * qinv) >> 20), c = w - r * qpr;
+                const int r = (int)(((uint64_t)(uint32_t)w * qinv) >> 32), c = w - r * qpr;
                 const uint4 v = s16[w];
                 uint32_t* d = (uint32_t*)(tile + r * SP + 16 * c);
                 d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
@@ -853,6 +853,8 @@ __global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, con
 }
 
 constexpr int kWavesWG = 4;   // waves per workgroup of eval_waves_kernel
+constexpr int kWideWG = 2;    // waves per workgroup of eval_wide_kernel (one individual each)
+constexpr int kWideMaxNC = 10; // eval_wide handles E <= 256 * kWideMaxNC
 
 template <int EWC, int PK>
 __global__ __launch_bounds__(64 * kWavesWG, 4) void eval_waves_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
@@ -951,6 +953,147 @@ __global__ __launch_bounds__(64 * kWavesWG, 4) void eval_waves_kernel(DevProblem
             }
         }
     }
+}
+
+// ---------------------------------------------------------------- eval_wide
+// The wave phase for instances too wide for eval_tile5's register-resident
+// correlation words (E > 448, e.g. the 2000-event synthetic instance), run
+// after eval_lanes_kernel<16> (which writes the per-student scv part):
+// wave = individual, lane l owns events e = 256 c + 4 l + k (k < 4) of every
+// 256-event chunk c < NC, so its slot/room bytes arrive as one dword per chunk
+// and its invariants (possibleRooms, studentNumber, upper-triangle words) as
+// 16-B vector loads from L2. Per-wave LDS workspace: event bitsets
+// B[45][BST] (BST = EW64 | 1 u64 words: an odd row stride spreads the 45 rows
+// over the banks) and packed u16 room-cell counters.
+//   hcv  = sum over cells of C(n, 2)                (Solution.cpp:148-150, ds_add_rtn)
+//        + sum_e [room_e not possible]              (:155-156)
+//        + sum_e sum_{w >= e/64} popcount(cupT[w][e] & B[slot_e][w])   (:151-153)
+//   scv += sum_e [slot_e % 9 == 8] studentNumber[e] (:93-96)
+template <int NC>
+__global__ __launch_bounds__(64 * kWideWG) void eval_wide_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
+                                                                 const uint8_t* __restrict__ room, int P,
+                                                                 int32_t* __restrict__ hcv_out,
+                                                                 int32_t* __restrict__ scv_io,
+                                                                 uint8_t* __restrict__ feas_out,
+                                                                 int32_t* __restrict__ pen_out, int BST, int WS) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int E = pb.E, R = pb.R, EW64 = pb.EW64;
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    uint8_t* ws = lds + (size_t)wv * WS;
+    uint64_t* B = (uint64_t*)ws;                              // [45][BST]
+    uint32_t* cnt = (uint32_t*)(B + kSlots * BST);            // packed u16 cell counters
+    // dword loads of the rows need 4-byte aligned rows
+    const bool al = (E & 3) == 0 && (((uintptr_t)slot | (uintptr_t)room) & 3) == 0;
+    const long GW = (long)gridDim.x * kWideWG;
+    for (long q = (long)blockIdx.x * kWideWG + wv; q < P; q += GW) {
+        const uint8_t* srow = slot + q * E;
+        const uint8_t* rrow = room + q * E;
+        uint32_t sv[NC], rv[NC];                              // bytes k = events 256c + 4 lane + k
+        int nv[NC];                                           // valid events of the lane in chunk c
+        bool bad = false;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int e0 = 256 * c + 4 * lane;
+            nv[c] = max(0, min(4, E - e0));
+            if (al && nv[c] == 4) {
+                sv[c] = *(const uint32_t*)(srow + e0);
+                rv[c] = *(const uint32_t*)(rrow + e0);
+            } else {
+                sv[c] = 0u; rv[c] = 0u;
+                for (int k = 0; k < nv[c]; ++k) {
+                    sv[c] |= (uint32_t)srow[e0 + k] << (8 * k);
+                    rv[c] |= (uint32_t)rrow[e0 + k] << (8 * k);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < nv[c]) bad |= ((sv[c] >> (8 * k)) & 0xFFu) >= (uint32_t)kSlots || ((rv[c] >> (8 * k)) & 0xFFu) >= (uint32_t)R;
+        }
+        const bool any_bad = __any(bad);
+        int h = 0, last = 0;
+        if (!any_bad) {
+            for (int i = lane; i < (WS >> 4); i += 64) ((uint4*)ws)[i] = make_uint4(0u, 0u, 0u, 0u);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int e0 = 256 * c + 4 * lane;
+                if (nv[c] == 0) continue;
+                uint64_t poss[4];
+                int sn[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    poss[k] = k < nv[c] ? pb.poss[e0 + k] : ~0ull;
+                    sn[k] = k < nv[c] ? pb.sn[e0 + k] : 0;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k < nv[c]) {
+                        const int e = e0 + k;
+                        const uint32_t s = (sv[c] >> (8 * k)) & 0xFFu, ro = (rv[c] >> (8 * k)) & 0xFFu;
+                        atomicOr((unsigned long long*)&B[s * (uint32_t)BST + (uint32_t)(e >> 6)], 1ull << (e & 63));
+                        const uint32_t cell = s * (uint32_t)R + ro, sh = (cell & 1u) << 4;
+                        h += (int)((atomicAdd(&cnt[cell >> 1], 1u << sh) >> sh) & 0xFFFFu);
+                        h += (int)(((poss[k] >> ro) & 1ull) ^ 1ull);
+                        last += ((kLastSlotMask >> s) & 1ull) ? sn[k] : 0;
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // correlated same-slot pairs: the words w >= 4c hold every upper-triangle
+            // bit of chunk c's events (bits j > e live in words >= e/64 >= 4c)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int e0 = 256 * c + 4 * lane;
+                if (nv[c] == 0) continue;
+                uint32_t boff[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) boff[k] = ((sv[c] >> (8 * k)) & 0xFFu) * (uint32_t)BST;
+#pragma unroll 2
+                for (int w = 4 * c; w < EW64; ++w) {
+                    const uint64_t* cw = pb.cupT + (size_t)w * E + e0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (k < nv[c]) h += __popcll(cw[k] & B[boff[k] + (uint32_t)w]);
+                }
+            }
+            h = wave_sum(h);
+            last = wave_sum(last);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (lane == 0) {
+            if (any_bad) {
+                hcv_out[q] = -1; scv_io[q] = -1; feas_out[q] = 0; pen_out[q] = -1;
+            } else {
+                const int s2 = scv_io[q] + last;
+                hcv_out[q] = h;
+                scv_io[q] = s2;
+                feas_out[q] = h == 0 ? 1 : 0;
+                pen_out[q] = h == 0 ? s2 : 1000000 + h;
+            }
+        }
+    }
+}
+
+struct WideLayout {
+    int BST, WS;
+    size_t lanes_bytes;
+};
+
+// LDS of the wide path: eval_lanes_kernel<16> tile + partials, per-wave workspace of eval_wide_kernel.
+static WideLayout wide_layout(int E, int R, int EW64) {
+    WideLayout L;
+    L.BST = EW64 | 1;
+    L.WS = (kSlots * L.BST * 8 + ((kSlots * R + 1) / 2) * 4 + 15) & ~15;
+    int sp = (E + 1 + 3) & ~3;
+    if (((sp >> 2) & 1) == 0) sp += 4;
+    L.lanes_bytes = (((size_t)64 * sp + 15) & ~(size_t)15) + 4 * (size_t)16 * 64;
+    return L;
 }
 
 // ---------------------------------------------------------------- eval_block
@@ -1057,6 +1200,9 @@ static int auto_variant(const tt_problem* p) {
     const int E = p->E, R = p->R;
     if (p->dev.EW64 <= 7 && E <= 32767 && tile5_layout(E, R, 8, false, false).bytes <= 80 * 1024) return 8;
     if (p->dev.EW64 <= 7 && tile4_layout(E, R, 4).bytes <= 64 * 1024) return 3;
+    const WideLayout WL = wide_layout(E, R, p->dev.EW64);
+    if (E <= 256 * kWideMaxNC && E <= 32767 && WL.lanes_bytes <= 160 * 1024 && (size_t)kWideWG * WL.WS <= 160 * 1024)
+        return 13;
     return (E <= 1024 && tile_layout(E, R).bytes <= 80 * 1024) ? 1 : 2;
 }
 
@@ -1069,7 +1215,7 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
     if (P > 0 && (!hcv || !scv || !feasible || !penalty)) { set_error("null output buffer"); return TT_ERR_INVALID; }
     const int ablate = variant >> 4;   // profiling-only phase switches (tile kernel)
     variant &= 15;
-    if (variant < 0 || variant > 10) { set_error("unknown eval variant"); return TT_ERR_INVALID; }
+    if (variant < 0 || variant > 13) { set_error("unknown eval variant"); return TT_ERR_INVALID; }
     if (P == 0) return TT_OK;
     rc = use_device(p);
     if (rc) return rc;
@@ -1167,6 +1313,43 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
             default: rc = TT_ERR_LIMIT; break;
         }
 #undef TT_TW
+        if (rc) return rc;
+    } else if (variant == 13) {
+        // wide path: eval_lanes<16> (tile of 64 rows, lane phase) then eval_wide (wave = individual)
+        const WideLayout WL = wide_layout(E, R, p->dev.EW64);
+        if (E > 256 * kWideMaxNC || E > 32767 || WL.lanes_bytes > 160 * 1024 || (size_t)kWideWG * WL.WS > 160 * 1024) {
+            set_error("instance outside the wide eval path");
+            return TT_ERR_LIMIT;
+        }
+        const int tiles = (P + 63) / 64;
+        {
+            int per_cu = 0;
+            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, eval_lanes_kernel<16>, 1024, WL.lanes_bytes));
+            const int grid = std::min(tiles, std::max(1, per_cu) * p->num_cus);
+            hipLaunchKernelGGL(eval_lanes_kernel<16>, dim3(grid), dim3(1024), WL.lanes_bytes, st, p->dev, slot, P, scv);
+        }
+        const size_t lds_w = (size_t)kWideWG * WL.WS;
+        auto launch_w = [&](auto kern) -> int {
+            int per_cu = 0;
+            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kWideWG, lds_w));
+            const int grid = (int)std::min<long>(((long)P + kWideWG - 1) / kWideWG, (long)std::max(1, per_cu) * p->num_cus);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kWideWG), lds_w, st, p->dev, slot, room, P, hcv, scv,
+                               feasible, penalty, WL.BST, WL.WS);
+            return TT_OK;
+        };
+        switch ((E + 255) / 256) {
+            case 1: rc = launch_w(eval_wide_kernel<1>); break;
+            case 2: rc = launch_w(eval_wide_kernel<2>); break;
+            case 3: rc = launch_w(eval_wide_kernel<3>); break;
+            case 4: rc = launch_w(eval_wide_kernel<4>); break;
+            case 5: rc = launch_w(eval_wide_kernel<5>); break;
+            case 6: rc = launch_w(eval_wide_kernel<6>); break;
+            case 7: rc = launch_w(eval_wide_kernel<7>); break;
+            case 8: rc = launch_w(eval_wide_kernel<8>); break;
+            case 9: rc = launch_w(eval_wide_kernel<9>); break;
+            case 10: rc = launch_w(eval_wide_kernel<10>); break;
+            default: rc = TT_ERR_LIMIT; break;
+        }
         if (rc) return rc;
     } else if (variant >= 5 && variant <= 8) {
         // 5/6: eval_tile5 with 4/8 waves, workspaces aliased on the tile, u32 cell

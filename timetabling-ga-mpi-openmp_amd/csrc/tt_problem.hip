@@ -134,7 +134,7 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     if (wch.empty()) wch.assign(8, 0);
     // the same records in student order, for eval_tile4: wave w of an NW-wave
     // workgroup takes a contiguous student range, balanced by record count.
-    // sch_part[kSchPart4 + w] (NW = 4) and sch_part[kSchPart8 + w] (NW = 8).
+    // sch_part[sch_part_base(NW) + w] for NW = 4, 8 and 16.
     std::vector<uint16_t> sch;
     std::vector<int32_t> stu_rec(S + 1, 0);
     if (E <= 32767) {
@@ -149,8 +149,8 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         }
     }
     std::vector<int32_t> sch_part(kSchPartLen, 0);
-    for (int nw : {4, 8}) {
-        const int base = nw == 4 ? kSchPart4 : kSchPart8;
+    for (int nw : {4, 8, 16}) {
+        const int base = sch_part_base(nw);
         const int total = stu_rec[S];
         int s = 0;
         for (int w = 0; w <= nw; w++) {
