@@ -853,7 +853,7 @@ __global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, con
 }
 
 constexpr int kWavesWG = 4;   // waves per workgroup of eval_waves_kernel
-constexpr int kWideWG = 2;    // waves per workgroup of eval_wide_kernel (one individual each)
+constexpr int kWideWG = 8;    // waves per workgroup of eval_wide_kernel (one individual each)
 constexpr int kWideMaxNC = 10; // eval_wide handles E <= 256 * kWideMaxNC
 
 template <int EWC, int PK>
@@ -959,42 +959,49 @@ __global__ __launch_bounds__(64 * kWavesWG, 4) void eval_waves_kernel(DevProblem
 // The wave phase for instances too wide for eval_tile5's register-resident
 // correlation words (E > 448, e.g. the 2000-event synthetic instance), run
 // after eval_lanes_kernel<16> (which writes the per-student scv part):
-// wave = individual, lane l owns events e = 256 c + 4 l + k (k < 4) of every
-// 256-event chunk c < NC, so its slot/room bytes arrive as one dword per chunk
-// and its invariants (possibleRooms, studentNumber, upper-triangle words) as
-// 16-B vector loads from L2. Per-wave LDS workspace: event bitsets
-// B[45][BST] (BST = EW64 | 1 u64 words: an odd row stride spreads the 45 rows
-// over the banks) and packed u16 room-cell counters.
+// wave = individual, NW waves (NW individuals) per workgroup, lane l owns
+// events e = 256 c + 4 l + k (k < 4) of every 256-event chunk c < NC, so its
+// slot/room bytes arrive as one dword per chunk and its invariants
+// (possibleRooms, studentNumber, upper-triangle words) as 16-B vector loads.
+// The upper-triangle words (E x EW64 / 2 u64, 256 KB at E = 2000) are the
+// dominant stream: the waves of a workgroup walk them in the same order and
+// meet at a barrier per chunk, so one wave's L2 fetch is the others' L1 hit.
+// Per-wave LDS workspace: event bitsets B[45][BST] (BST = EW64 | 1 u64 words:
+// an odd row stride spreads the 45 rows over the banks) and packed u16
+// room-cell counters.
 //   hcv  = sum over cells of C(n, 2)                (Solution.cpp:148-150, ds_add_rtn)
 //        + sum_e [room_e not possible]              (:155-156)
 //        + sum_e sum_{w >= e/64} popcount(cupT[w][e] & B[slot_e][w])   (:151-153)
 //   scv += sum_e [slot_e % 9 == 8] studentNumber[e] (:93-96)
-template <int NC>
-__global__ __launch_bounds__(64 * kWideWG) void eval_wide_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
-                                                                 const uint8_t* __restrict__ room, int P,
-                                                                 int32_t* __restrict__ hcv_out,
-                                                                 int32_t* __restrict__ scv_io,
-                                                                 uint8_t* __restrict__ feas_out,
-                                                                 int32_t* __restrict__ pen_out, int BST, int WS) {
+template <int NC, int NW>
+__global__ __launch_bounds__(64 * NW) void eval_wide_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
+                                                            const uint8_t* __restrict__ room, int P,
+                                                            int32_t* __restrict__ hcv_out,
+                                                            int32_t* __restrict__ scv_io,
+                                                            uint8_t* __restrict__ feas_out,
+                                                            int32_t* __restrict__ pen_out, int BST, int WS,
+                                                            int ablate) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int E = pb.E, R = pb.R, EW64 = pb.EW64;
     const int lane = threadIdx.x & 63, wv = wave_id();
     uint8_t* ws = lds + (size_t)wv * WS;
     uint64_t* B = (uint64_t*)ws;                              // [45][BST]
     uint32_t* cnt = (uint32_t*)(B + kSlots * BST);            // packed u16 cell counters
-    // dword loads of the rows need 4-byte aligned rows
+    // dword row loads and 16-B upper-triangle loads need E % 4 == 0 and aligned rows
     const bool al = (E & 3) == 0 && (((uintptr_t)slot | (uintptr_t)room) & 3) == 0;
-    const long GW = (long)gridDim.x * kWideWG;
-    for (long q = (long)blockIdx.x * kWideWG + wv; q < P; q += GW) {
-        const uint8_t* srow = slot + q * E;
-        const uint8_t* rrow = room + q * E;
+    const int groups = (P + NW - 1) / NW;
+    for (int g = blockIdx.x; g < groups; g += gridDim.x) {     // every wave runs every barrier
+        const long q = (long)g * NW + wv;
+        const bool act = q < P;
         uint32_t sv[NC], rv[NC];                              // bytes k = events 256c + 4 lane + k
         int nv[NC];                                           // valid events of the lane in chunk c
         bool bad = false;
+        const uint8_t* srow = slot + (act ? q : 0) * E;
+        const uint8_t* rrow = room + (act ? q : 0) * E;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             const int e0 = 256 * c + 4 * lane;
-            nv[c] = max(0, min(4, E - e0));
+            nv[c] = act ? max(0, min(4, E - e0)) : 0;
             if (al && nv[c] == 4) {
                 sv[c] = *(const uint32_t*)(srow + e0);
                 rv[c] = *(const uint32_t*)(rrow + e0);
@@ -1009,9 +1016,9 @@ __global__ __launch_bounds__(64 * kWideWG) void eval_wide_kernel(DevProblem pb, 
             for (int k = 0; k < 4; ++k)
                 if (k < nv[c]) bad |= ((sv[c] >> (8 * k)) & 0xFFu) >= (uint32_t)kSlots || ((rv[c] >> (8 * k)) & 0xFFu) >= (uint32_t)R;
         }
-        const bool any_bad = __any(bad);
+        const bool work = act && !__any(bad);                 // wave-uniform
         int h = 0, last = 0;
-        if (!any_bad) {
+        if (work && !(ablate & 1)) {
             for (int i = lane; i < (WS >> 4); i += 64) ((uint4*)ws)[i] = make_uint4(0u, 0u, 0u, 0u);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1043,31 +1050,44 @@ __global__ __launch_bounds__(64 * kWideWG) void eval_wide_kernel(DevProblem pb, 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // correlated same-slot pairs: the words w >= 4c hold every upper-triangle
-            // bit of chunk c's events (bits j > e live in words >= e/64 >= 4c)
+        }
+        // correlated same-slot pairs: the words w >= 4c hold every upper-triangle
+        // bit of chunk c's events (bits j > e live in words >= e/64 >= 4c)
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                const int e0 = 256 * c + 4 * lane;
-                if (nv[c] == 0) continue;
+        for (int c = 0; c < NC; ++c) {
+            __syncthreads();                                  // keep the group's waves on the same words
+            const int e0 = 256 * c + 4 * lane;
+            if (work && nv[c] > 0 && !(ablate & 2)) {
                 uint32_t boff[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) boff[k] = ((sv[c] >> (8 * k)) & 0xFFu) * (uint32_t)BST;
+                if (al) {                                     // nv[c] == 4; 32-B aligned words
+#pragma unroll 4
+                    for (int w = 4 * c; w < EW64; ++w) {
+                        const uint4* cw = (const uint4*)(pb.cupT + (size_t)w * E + e0);
+                        const uint4 x = cw[0], y = cw[1];
+                        h += __popcll((((uint64_t)x.y << 32) | x.x) & B[boff[0] + (uint32_t)w]);
+                        h += __popcll((((uint64_t)x.w << 32) | x.z) & B[boff[1] + (uint32_t)w]);
+                        h += __popcll((((uint64_t)y.y << 32) | y.x) & B[boff[2] + (uint32_t)w]);
+                        h += __popcll((((uint64_t)y.w << 32) | y.z) & B[boff[3] + (uint32_t)w]);
+                    }
+                } else {
 #pragma unroll 2
-                for (int w = 4 * c; w < EW64; ++w) {
-                    const uint64_t* cw = pb.cupT + (size_t)w * E + e0;
+                    for (int w = 4 * c; w < EW64; ++w) {
+                        const uint64_t* cw = pb.cupT + (size_t)w * E + e0;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        if (k < nv[c]) h += __popcll(cw[k] & B[boff[k] + (uint32_t)w]);
+                        for (int k = 0; k < 4; ++k)
+                            if (k < nv[c]) h += __popcll(cw[k] & B[boff[k] + (uint32_t)w]);
+                    }
                 }
             }
+        }
+        if (work) {
             h = wave_sum(h);
             last = wave_sum(last);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        if (lane == 0) {
-            if (any_bad) {
+        if (act && lane == 0) {
+            if (!work) {
                 hcv_out[q] = -1; scv_io[q] = -1; feas_out[q] = 0; pen_out[q] = -1;
             } else {
                 const int s2 = scv_io[q] + last;
@@ -1077,6 +1097,7 @@ __global__ __launch_bounds__(64 * kWideWG) void eval_wide_kernel(DevProblem pb, 
                 pen_out[q] = h == 0 ? s2 : 1000000 + h;
             }
         }
+        __syncthreads();                                      // workspaces are reused by the next group
     }
 }
 
@@ -1201,7 +1222,7 @@ static int auto_variant(const tt_problem* p) {
     if (p->dev.EW64 <= 7 && E <= 32767 && tile5_layout(E, R, 8, false, false).bytes <= 80 * 1024) return 8;
     if (p->dev.EW64 <= 7 && tile4_layout(E, R, 4).bytes <= 64 * 1024) return 3;
     const WideLayout WL = wide_layout(E, R, p->dev.EW64);
-    if (E <= 256 * kWideMaxNC && E <= 32767 && WL.lanes_bytes <= 160 * 1024 && (size_t)kWideWG * WL.WS <= 160 * 1024)
+    if (E <= 256 * kWideMaxNC && E <= 32767 && WL.lanes_bytes <= 160 * 1024 && (size_t)(kWideWG / 2) * WL.WS <= 160 * 1024)
         return 13;
     return (E <= 1024 && tile_layout(E, R).bytes <= 80 * 1024) ? 1 : 2;
 }
@@ -1317,7 +1338,7 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
     } else if (variant == 13) {
         // wide path: eval_lanes<16> (tile of 64 rows, lane phase) then eval_wide (wave = individual)
         const WideLayout WL = wide_layout(E, R, p->dev.EW64);
-        if (E > 256 * kWideMaxNC || E > 32767 || WL.lanes_bytes > 160 * 1024 || (size_t)kWideWG * WL.WS > 160 * 1024) {
+        if (E > 256 * kWideMaxNC || E > 32767 || WL.lanes_bytes > 160 * 1024 || (size_t)(kWideWG / 2) * WL.WS > 160 * 1024) {
             set_error("instance outside the wide eval path");
             return TT_ERR_LIMIT;
         }
@@ -1328,28 +1349,24 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
             const int grid = std::min(tiles, std::max(1, per_cu) * p->num_cus);
             hipLaunchKernelGGL(eval_lanes_kernel<16>, dim3(grid), dim3(1024), WL.lanes_bytes, st, p->dev, slot, P, scv);
         }
-        const size_t lds_w = (size_t)kWideWG * WL.WS;
+        // 8 individuals per workgroup, or 4 where 8 workspaces exceed the LDS
+        const int NWW = (size_t)kWideWG * WL.WS <= 160 * 1024 ? kWideWG : kWideWG / 2;
+        const size_t lds_w = (size_t)NWW * WL.WS;
         auto launch_w = [&](auto kern) -> int {
             int per_cu = 0;
-            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kWideWG, lds_w));
-            const int grid = (int)std::min<long>(((long)P + kWideWG - 1) / kWideWG, (long)std::max(1, per_cu) * p->num_cus);
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kWideWG), lds_w, st, p->dev, slot, room, P, hcv, scv,
-                               feasible, penalty, WL.BST, WL.WS);
+            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NWW, lds_w));
+            const int grid = (int)std::min<long>(((long)P + NWW - 1) / NWW, (long)std::max(1, per_cu) * p->num_cus);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NWW), lds_w, st, p->dev, slot, room, P, hcv, scv,
+                               feasible, penalty, WL.BST, WL.WS, ablate);
             return TT_OK;
         };
+#define TT_WD(NC) \
+    case NC: rc = NWW == kWideWG ? launch_w(eval_wide_kernel<NC, kWideWG>) : launch_w(eval_wide_kernel<NC, kWideWG / 2>); break;
         switch ((E + 255) / 256) {
-            case 1: rc = launch_w(eval_wide_kernel<1>); break;
-            case 2: rc = launch_w(eval_wide_kernel<2>); break;
-            case 3: rc = launch_w(eval_wide_kernel<3>); break;
-            case 4: rc = launch_w(eval_wide_kernel<4>); break;
-            case 5: rc = launch_w(eval_wide_kernel<5>); break;
-            case 6: rc = launch_w(eval_wide_kernel<6>); break;
-            case 7: rc = launch_w(eval_wide_kernel<7>); break;
-            case 8: rc = launch_w(eval_wide_kernel<8>); break;
-            case 9: rc = launch_w(eval_wide_kernel<9>); break;
-            case 10: rc = launch_w(eval_wide_kernel<10>); break;
+            TT_WD(1) TT_WD(2) TT_WD(3) TT_WD(4) TT_WD(5) TT_WD(6) TT_WD(7) TT_WD(8) TT_WD(9) TT_WD(10)
             default: rc = TT_ERR_LIMIT; break;
         }
+#undef TT_WD
         if (rc) return rc;
     } else if (variant >= 5 && variant <= 8) {
         // 5/6: eval_tile5 with 4/8 waves, workspaces aliased on the tile, u32 cell
