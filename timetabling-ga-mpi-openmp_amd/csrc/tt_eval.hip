@@ -699,7 +699,8 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
             const bool any_bad = __any(smax >= (uint32_t)kSlots || rmax >= (uint32_t)R);
             int h = 0, last = 0;
             if (!any_bad) {
-                for (int c = lane; c < (L.WS >> 4); c += 64) ((uint4*)ws)[c] = make_uint4(0u, 0u, 0u, 0u);
+                if (!(ablate & 32))
+                    for (int c = lane; c < (L.WS >> 4); c += 64) ((uint4*)ws)[c] = make_uint4(0u, 0u, 0u, 0u);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -707,9 +708,10 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
                 for (int r = 0; r < EWC; ++r) {
                     if (r < EWC - 1 || !last_partial || lane + 64 * r < E) {
                         const uint32_t s = sv[r], ro = rv[r];
-                        atomicOr((unsigned long long*)&B[s * EWC + r], 1ull << lane);
+                        if (!(ablate & 8)) atomicOr((unsigned long long*)&B[s * EWC + r], 1ull << lane);
                         const uint32_t cell = s * (uint32_t)R + ro;
-                        if constexpr (CNT32) {
+                        if (ablate & 16) {
+                        } else if constexpr (CNT32) {
                             h += (int)atomicAdd(&cnt[cell], 1u);                        // Solution.cpp:148-150
                         } else {
                             const uint32_t sh = (cell & 1u) << 4;
@@ -1234,7 +1236,10 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
     int rc = check_pop_args(p, P, slot, room);
     if (rc) return rc;
     if (P > 0 && (!hcv || !scv || !feasible || !penalty)) { set_error("null output buffer"); return TT_ERR_INVALID; }
-    const int ablate = variant >> 4;   // profiling-only phase switches (tile kernel)
+    // profiling-only phase switches (results invalid): 1 lane phase, 2 wave phase, 4 correlation
+    // words, 8 B-bitset atomics, 16 cell-counter atomics, 32 workspace zeroing (eval_tile5);
+    // 1 atomics + zeroing, 2 correlation words (eval_wide)
+    const int ablate = variant >> 4;
     variant &= 15;
     if (variant < 0 || variant > 13) { set_error("unknown eval variant"); return TT_ERR_INVALID; }
     if (P == 0) return TT_OK;
