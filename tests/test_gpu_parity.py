@@ -254,3 +254,27 @@ def test_local_search_random_vs_oracle(orc):
     dp.local_search(s, r, g, 3000)
     es, er, eg = o.local_search(es, er, eg, 3000)
     assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg)
+
+
+def test_local_search_crowded_slots_redo(orc):
+    """tt_local_search runs a first launch whose matcher tasks hold 64 events per
+    slot; an individual whose trial touches a slot with more events is redone
+    from its untouched input by the full-size launch. Crowded individuals (70 to
+    150 events in one slot) mixed with ordinary ones must match the oracle
+    exactly, with the device status clean."""
+    inst = ttga.generate(400, 10, 5, 200, seed=23)
+    dp = native.DeviceProblem(inst)
+    o = orc.problem(inst)
+    P = 12
+    s0, _, _ = o.random_init(ttga.population_seeds(808, P))
+    rng = np.random.default_rng(3)
+    for k, n in ((1, 70), (4, 100), (7, 150), (10, 65)):
+        idx = rng.choice(inst.E, size=n, replace=False)
+        s0[k, idx] = 3 + k                                # one crowded slot
+    r0 = o.assign_rooms(s0)
+    seeds = ttga.population_seeds(909, P)
+    s, r, g = dev(s0), dev(r0), dev(seeds)
+    dp.local_search(s, r, g, 300)
+    es, er, eg = o.local_search(s0, r0, seeds, 300)
+    assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg)
+    assert dp.status() == 0

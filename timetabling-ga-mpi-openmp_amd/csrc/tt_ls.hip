@@ -23,6 +23,12 @@
 namespace ttga {
 
 constexpr int kLsTasks = 3;
+// Two launches per call: the first sizes each of the 3 matcher tasks for 64
+// events per slot (8 KB of LDS per wave at E = 400 instead of 14.6 KB, so about
+// twice the waves per CU); an individual whose trial puts more than 64 events
+// into a touched slot stops there, untouched in HBM, and is redone from its
+// input by the second launch with tasks sized for kMaxSlotEvents.
+constexpr int kLsCapSmall = 64;
 
 struct LsLayout {
     size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, task;
@@ -31,7 +37,8 @@ struct LsLayout {
     size_t bytes;
 };
 
-__host__ __device__ inline LsLayout ls_layout(int E, int R, int EW) {
+// cap: events per matcher task (kLsCapSmall for the first launch, kMaxSlotEvents for the redo launch)
+__host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap) {
     LsLayout L;
     size_t b = 0;
     auto al = [&](size_t a) { b = (b + a - 1) & ~(a - 1); };
@@ -44,7 +51,7 @@ __host__ __device__ inline LsLayout ls_layout(int E, int R, int EW) {
     L.rp = b; b += 4 * (size_t)kSlots;
     L.hist = b; b += 2 * (size_t)kSlots * R;
     al(4); L.misc = b; b += 4 * 32;
-    L.NT = E < kMaxSlotEvents ? E : kMaxSlotEvents;
+    L.NT = E < cap ? E : cap;
     size_t tb = 11 * (size_t)L.NT + 1 + 4 * (size_t)R;   // pl, ev, mr, (pad), hist, rm, dr
     L.task_bytes = (tb + 15) & ~(size_t)15;
     al(16); L.task = b; b += kLsTasks * L.task_bytes;
@@ -173,19 +180,25 @@ __device__ __forceinline__ void scv_terms(const LsState& S, int e, bool nb, int&
 }
 
 // Builds NB[k] for the touched slots and re-matches them, one lane per slot.
-__device__ __forceinline__ void build_and_match(LsState& S) {
+__device__ __forceinline__ bool build_and_match(LsState& S) {
     const int EW = S.EW;
-    for (int k = 0; k < S.nts; ++k) {
+    // static indices into ts/mv_e/mv_t (unrolled to 3): a runtime index would
+    // force the whole LsState into scratch and every LDS pointer through flat loads
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (k >= S.nts) break;
         const int t = S.ts[k];
         for (int w = S.lane; w < EW; w += 64) {
             uint64_t x = S.B[(size_t)t * EW + w];
-            for (int q = 0; q < S.nmv; ++q) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
                 const int e = S.mv_e[q];
-                if (S.sl[e] == t && (e >> 6) == w) x &= ~(1ull << (e & 63));
+                if (q < S.nmv && S.sl[e] == t && (e >> 6) == w) x &= ~(1ull << (e & 63));
             }
-            for (int q = 0; q < S.nmv; ++q) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
                 const int e = S.mv_e[q];
-                if (S.mv_t[q] == t && (e >> 6) == w) x |= 1ull << (e & 63);
+                if (q < S.nmv && S.mv_t[q] == t && (e >> 6) == w) x |= 1ull << (e & 63);
             }
             S.NB[(size_t)k * EW + w] = x;
         }
@@ -202,16 +215,18 @@ __device__ __forceinline__ void build_and_match(LsState& S) {
             while (x) {
                 const int e = 64 * w + __builtin_ctzll(x);
                 x &= x - 1;
-                if (N < kMaxSlotEvents) { T.ev[N] = (uint16_t)e; T.pl[N] = S.pb.poss[e]; }
+                if (N < S.NT) { T.ev[N] = (uint16_t)e; T.pl[N] = S.pb.poss[e]; }
                 else over = true;
                 ++N;
             }
         }
         for (int r = 0; r < S.R; ++r) T.hist[r] = 0;
         int pairs = 0;
-        if (over) {
+        if (over && S.NT < kMaxSlotEvents && S.NT < S.E) {
+            S.misc[3] = 1;                                          // first launch: redo with full tasks
+        } else if (over) {
             atomicOr(S.pb.status, 1);
-            for (int i = 0; i < kMaxSlotEvents; ++i) S.nrr[T.ev[i]] = 0xFF;
+            for (int i = 0; i < S.NT; ++i) S.nrr[T.ev[i]] = 0xFF;
         } else if (N > 0) {
             if (N <= 64) match_slot<1>(S.R, T.ev, T.pl, N, T.mr, T.rm, T.dr, S.nrr);
             else match_slot<4>(S.R, T.ev, T.pl, N, T.mr, T.rm, T.dr, S.nrr);
@@ -224,6 +239,7 @@ __device__ __forceinline__ void build_and_match(LsState& S) {
         S.misc[k] = pairs;
     }
     wave_sync();
+    return S.misc[3] != 0;
 }
 
 // events of neighbour slot k: copy rooms between rr and nrr
@@ -245,15 +261,21 @@ __device__ __forceinline__ void sync_rooms(LsState& S, bool accept) {
 
 __device__ __forceinline__ void accept(LsState& S) {
     sync_rooms(S, true);
-    for (int k = 0; k < S.nts; ++k) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (k >= S.nts) break;
         const int t = S.ts[k];
         for (int w = S.lane; w < S.EW; w += 64) S.B[(size_t)t * S.EW + w] = S.NB[(size_t)k * S.EW + w];
         const LsTask T = get_task(S, k);
         for (int r = S.lane; r < S.R; r += 64) S.hist[t * S.R + r] = T.hist[r];
     }
     if (S.lane == 0) {
-        for (int k = 0; k < S.nts; ++k) S.rp[S.ts[k]] = S.misc[k];
-        for (int q = 0; q < S.nmv; ++q) S.sl[S.mv_e[q]] = (uint8_t)S.mv_t[q];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            if (k < S.nts) S.rp[S.ts[k]] = S.misc[k];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            if (q < S.nmv) S.sl[S.mv_e[q]] = (uint8_t)S.mv_t[q];
     }
     wave_sync();
 }
@@ -299,14 +321,21 @@ __device__ __forceinline__ bool feasible_now(const LsState& S) {
     return wave_sum(h) == 0;
 }
 
+// CAP = matcher task capacity. redo_out (first launch): set to 1 for an
+// individual that overflowed a task, whose HBM row and stream are then left
+// as they were. redo_in (second launch): only flagged individuals run.
+template <int CAP>
 __global__ __launch_bounds__(64) void local_search_kernel(DevProblem pb, uint8_t* __restrict__ slot,
                                                           uint8_t* __restrict__ room, int64_t* __restrict__ rng,
-                                                          int P, int max_steps, double p1, double p2, double p3) {
+                                                          int P, int max_steps, double p1, double p2, double p3,
+                                                          uint8_t* __restrict__ redo_out,
+                                                          const uint8_t* __restrict__ redo_in) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int E = pb.E, R = pb.R, EW = pb.EW64;
     const int lane = threadIdx.x;
     const long p = blockIdx.x;
-    const LsLayout L = ls_layout(E, R, EW);
+    if (redo_in && !redo_in[p]) return;
+    const LsLayout L = ls_layout(E, R, EW, CAP);
     LsState S;
     S.pb = pb; S.E = E; S.R = R; S.EW = EW; S.lane = lane;
     S.sl = lds + L.sl; S.rr = lds + L.rr; S.nrr = lds + L.nrr;
@@ -318,6 +347,7 @@ __global__ __launch_bounds__(64) void local_search_kernel(DevProblem pb, uint8_t
     S.task_bytes = (int)L.task_bytes;
     S.NT = L.NT;
     S.nmv = 0; S.nts = 0;
+    if (lane == 0) S.misc[3] = 0;
 
     // ---- load the individual, derive the incremental state
     bool bad = false;
@@ -385,7 +415,7 @@ __global__ __launch_bounds__(64) void local_search_kernel(DevProblem pb, uint8_t
                 if (pm_next(st) < p1) {
                     step++;
                     set_move(S, 1, ei, t, 0);
-                    build_and_match(S);
+                    if (build_and_match(S)) goto redo;
                     const int n = eah_nb(S, ei) + S.misc[task_of(S, t_orig)];
                     const int c = eah_cur(S, ei) + S.rp[t];
                     if (n < c) { accept(S); evc = 0; better = true; break; }
@@ -401,7 +431,7 @@ __global__ __launch_bounds__(64) void local_search_kernel(DevProblem pb, uint8_t
                         const int ej = S.evl[j];
                         const int c = eah_cur(S, ei) + eah_cur(S, ej);
                         set_move(S, 2, ei, ej, 0);
-                        build_and_match(S);
+                        if (build_and_match(S)) goto redo;
                         const int n = eah_nb(S, ei) + eah_nb(S, ej);
                         if (n < c) { accept(S); evc = 0; better = true; break; }
                         sync_rooms(S, false);
@@ -419,7 +449,7 @@ __global__ __launch_bounds__(64) void local_search_kernel(DevProblem pb, uint8_t
                             step++;
                             const int c = eah_cur(S, ei) + eah_cur(S, ej) + eah_cur(S, ek);
                             set_move(S, 3, ei, ej, ek);
-                            build_and_match(S);
+                            if (build_and_match(S)) goto redo;
                             const int n = eah_nb(S, ei) + eah_nb(S, ej) + eah_nb(S, ek);
                             if (n < c) { accept(S); evc = 0; better = true; break; }
                             sync_rooms(S, false);
@@ -429,7 +459,7 @@ __global__ __launch_bounds__(64) void local_search_kernel(DevProblem pb, uint8_t
                             step++;
                             const int c = eah_cur(S, ei) + eah_cur(S, ek) + eah_cur(S, ej);
                             set_move(S, 3, ei, ek, ej);
-                            build_and_match(S);
+                            if (build_and_match(S)) goto redo;
                             const int n = eah_nb(S, ei) + eah_nb(S, ek) + eah_nb(S, ej);
                             if (n < c) { accept(S); evc = 0; better = true; break; }
                             sync_rooms(S, false);
@@ -456,7 +486,7 @@ __global__ __launch_bounds__(64) void local_search_kernel(DevProblem pb, uint8_t
                 if (pm_next(st) < p1) {
                     step++;
                     set_move(S, 1, ei, t, 0);
-                    build_and_match(S);
+                    if (build_and_match(S)) goto redo;
                     if (eah_nb(S, ei) == 0) {
                         int es_n, scs_n;
                         scv_terms(S, ei, true, es_n, scs_n);
@@ -473,7 +503,7 @@ __global__ __launch_bounds__(64) void local_search_kernel(DevProblem pb, uint8_t
                         step++;
                         const int ej = S.evl[j];
                         set_move(S, 2, ei, ej, 0);
-                        build_and_match(S);
+                        if (build_and_match(S)) goto redo;
                         if (eah_nb(S, ei) + eah_nb(S, ej) == 0) {
                             int es_ni, scs_ni, es_nj, scs_nj, es_cj, scs_cj;
                             scv_terms(S, ei, true, es_ni, scs_ni);
@@ -499,7 +529,7 @@ __global__ __launch_bounds__(64) void local_search_kernel(DevProblem pb, uint8_t
                             step++;
                             const int a = order ? ek : ej, b = order ? ej : ek;
                             set_move(S, 3, ei, a, b);
-                            build_and_match(S);
+                            if (build_and_match(S)) goto redo;
                             if (eah_nb(S, ei) + eah_nb(S, a) + eah_nb(S, b) == 0) {
                                 int es_ni, scs_ni, es_na, scs_na, es_nb, scs_nb, es_ca, scs_ca, es_cb, scs_cb;
                                 scv_terms(S, ei, true, es_ni, scs_ni);
@@ -529,6 +559,9 @@ __global__ __launch_bounds__(64) void local_search_kernel(DevProblem pb, uint8_t
         room[p * E + e] = S.rr[e];
     }
     if (lane == 0) rng[p] = st;
+    return;
+redo:
+    if (lane == 0) redo_out[p] = 1;
 }
 
 }  // namespace ttga
@@ -542,9 +575,24 @@ extern "C" int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room
     if (!rng) { set_error("null rng buffer"); return TT_ERR_INVALID; }
     if (max_steps < 0) { set_error("negative max_steps"); return TT_ERR_INVALID; }
     if ((rc = use_device(p))) return rc;
-    const LsLayout L = ls_layout(p->E, p->R, p->dev.EW64);
-    if (L.bytes > 160 * 1024) { set_error("instance too large for the local-search kernel"); return TT_ERR_LIMIT; }
-    hipLaunchKernelGGL(local_search_kernel, dim3(P), dim3(64), L.bytes, (hipStream_t)stream, p->dev, slot, room, rng,
-                       P, max_steps, p1, p2, p3);
-    return check_hip(hipGetLastError(), "local_search launch");
+    const LsLayout Lf = ls_layout(p->E, p->R, p->dev.EW64, kMaxSlotEvents);
+    if (Lf.bytes > 160 * 1024) { set_error("instance too large for the local-search kernel"); return TT_ERR_LIMIT; }
+    hipStream_t st = (hipStream_t)stream;
+    if (p->E <= kLsCapSmall) {                      // no slot can exceed the small tasks
+        hipLaunchKernelGGL(local_search_kernel<kMaxSlotEvents>, dim3(P), dim3(64), Lf.bytes, st, p->dev, slot, room,
+                           rng, P, max_steps, p1, p2, p3, (uint8_t*)nullptr, (const uint8_t*)nullptr);
+        return check_hip(hipGetLastError(), "local_search launch");
+    }
+    const LsLayout Ls = ls_layout(p->E, p->R, p->dev.EW64, kLsCapSmall);
+    uint8_t* redo = nullptr;
+    TT_HIP(hipMallocAsync((void**)&redo, (size_t)P, st));
+    TT_HIP(hipMemsetAsync(redo, 0, (size_t)P, st));
+    hipLaunchKernelGGL(local_search_kernel<kLsCapSmall>, dim3(P), dim3(64), Ls.bytes, st, p->dev, slot, room, rng, P,
+                       max_steps, p1, p2, p3, redo, (const uint8_t*)nullptr);
+    TT_HIP(hipGetLastError());
+    hipLaunchKernelGGL(local_search_kernel<kMaxSlotEvents>, dim3(P), dim3(64), Lf.bytes, st, p->dev, slot, room, rng,
+                       P, max_steps, p1, p2, p3, (uint8_t*)nullptr, (const uint8_t*)redo);
+    TT_HIP(hipGetLastError());
+    TT_HIP(hipFreeAsync(redo, st));
+    return TT_OK;
 }
