@@ -31,7 +31,7 @@ constexpr int kLsTasks = 3;
 constexpr int kLsCapSmall = 64;
 
 struct LsLayout {
-    size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, task;
+    size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, cnt, task;
     size_t task_bytes;
     int NT;              // events per matcher task (min(E, 256))
     size_t bytes;
@@ -51,6 +51,7 @@ __host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap) {
     L.rp = b; b += 4 * (size_t)kSlots;
     L.hist = b; b += 2 * (size_t)kSlots * R;
     al(4); L.misc = b; b += 4 * 32;
+    L.cnt = b; b += 4 * (size_t)kMaxRooms;
     L.NT = E < cap ? E : cap;
     size_t tb = 11 * (size_t)L.NT + 1 + 4 * (size_t)R;   // pl, ev, mr, (pad), hist, rm, dr
     L.task_bytes = (tb + 15) & ~(size_t)15;
@@ -79,7 +80,8 @@ struct LsState {
     uint64_t *B, *NB;
     int32_t* rp;
     uint16_t* hist;
-    int32_t* misc;       // [0..2] neighbour room pairs per task
+    int32_t* misc;       // [0..2] neighbour room pairs per task, [3] redo flag, [4..6] events per task
+    uint32_t* cnt;       // [R] room counters of the task being read out
     uint8_t* task_base;
     int task_bytes, NT;
     // neighbour description (wave-uniform)
@@ -179,7 +181,102 @@ __device__ __forceinline__ void scv_terms(const LsState& S, int e, bool nb, int&
     scs = wave_sum(b);
 }
 
-// Builds NB[k] for the touched slots and re-matches them, one lane per slot.
+// Wave matcher for one touched slot of N <= 64 events, the same search as
+// match_slot<1> (tt_match.h, Solution.cpp:772-891), with its state in
+// registers: lane i holds event i's possible-room mask (pl) and matched room
+// (mr); lane j holds room j's matched event (rm), search dad (dr) and the mask
+// of the slot's events that may use it (ev_of_room); the seen/fringe sets are
+// wave-uniform (scalar) bitsets. The search expands every fringe event before
+// any room, so its first stage -- all unmatched events in ascending order --
+// is closed-form: the rooms seen are those with an unmatched candidate event,
+// and room j's dad is the lowest unmatched event that may use it. Only the
+// room stage (ascending rooms, a matched room's event expanded at once) walks
+// step by step.
+__device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev, uint64_t pl) {
+    const int lane = S.lane, R = S.R;
+    constexpr uint32_t NONE = 0xFFu;
+    const bool act = lane < N;
+    const uint32_t pl_lo = (uint32_t)pl, pl_hi = (uint32_t)(pl >> 32);
+    // transpose: ev_of_room (lane j) = the events whose possible rooms include j
+    uint64_t eor = 0;
+    for (int j = 0; j < R; ++j) {
+        const uint64_t b = __ballot(act && ((pl >> j) & 1ull));
+        if (lane == j) eor = b;
+    }
+    uint32_t mr = NONE, rm = 0, dr = 0;
+    uint64_t unm = N >= 64 ? ~0ull : ((1ull << N) - 1ull);
+    uint64_t rmatched = 0;
+    for (;;) {
+        // stage 1 (closed form): expand all unmatched events, ascending
+        const uint64_t cand = eor & unm;
+        uint64_t sr = __ballot(lane < R && cand != 0ull), fr = sr, se = unm;
+        if (cand) dr = (uint32_t)__builtin_ctzll(cand);
+        // stage 2: fringe rooms ascending; a matched room's event is expanded at once
+        int sink = -1;
+        while (fr) {
+            const int j = __builtin_ctzll(fr);
+            fr &= fr - 1;
+            if (!((rmatched >> j) & 1ull)) { sink = j; break; }     // free room: the path is fixed
+            const int i2 = __builtin_amdgcn_readlane((int)rm, j);
+            const uint64_t bi = 1ull << i2;
+            if (se & bi) continue;
+            se |= bi;
+            const uint32_t mi = (uint32_t)__builtin_amdgcn_readlane((int)mr, i2);
+            const uint64_t own = mi != NONE ? (1ull << mi) : 0ull;
+            const uint64_t pli = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)pl_hi, i2) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)pl_lo, i2);
+            const uint64_t nr = pli & ~sr & ~own;
+            sr |= nr;
+            fr |= nr;
+            if ((nr >> lane) & 1ull) dr = (uint32_t)i2;
+        }
+        if (sink < 0) break;
+        // maxMatching augmentation (Solution.cpp:836-849)
+        int j = sink;
+        for (;;) {
+            const int i = __builtin_amdgcn_readlane((int)dr, j);
+            const uint32_t prev = (uint32_t)__builtin_amdgcn_readlane((int)mr, i);
+            if (lane == i) mr = (uint32_t)j;
+            if (lane == j) rm = (uint32_t)i;
+            rmatched |= 1ull << j;
+            if (prev == NONE) { unm &= ~(1ull << i); break; }
+            j = (int)prev;
+        }
+    }
+    // read-out (Solution.cpp:802-830): unplaced events, ascending, take the first
+    // free possible room, else the first possible room; one with no possible room
+    // keeps lessBusy carried over from the previous unplaced event (initially 0)
+    const bool un = act && mr == NONE;
+    uint32_t v = 0;
+    if (un && pl) {
+        v = (uint32_t)__builtin_ctzll(pl);
+        if ((rmatched >> v) & 1ull) {
+            const uint64_t fr2 = pl & ~rmatched;
+            if (fr2) v = (uint32_t)__builtin_ctzll(fr2);
+        }
+    }
+    const uint64_t carriers = __ballot(un && pl != 0ull);
+    const uint64_t below = carriers & ((1ull << lane) - 1ull);
+    const int src = below ? 63 - __builtin_clzll(below) : lane;
+    const uint32_t carried = (uint32_t)__shfl((int)v, src, 64);
+    const uint32_t r = !un ? mr : (pl ? v : (below ? carried : 0u));
+    const LsTask T = get_task(S, k);
+    if (lane < R) S.cnt[lane] = 0u;
+    wave_sync();
+    int pr = 0;
+    if (act) {
+        S.nrr[ev] = (uint8_t)r;
+        pr = (int)atomicAdd(&S.cnt[r], 1u);            // pairs of events sharing a room
+    }
+    wave_sync();
+    if (lane < R) T.hist[lane] = (uint16_t)S.cnt[lane];
+    pr = wave_sum(pr);
+    if (lane == 0) S.misc[k] = pr;
+}
+
+// Builds NB[k] for the touched slots and re-matches them: lane k lists the
+// events of slot k, then the wave matcher runs the slots one after another
+// (the lane-serial match_slot<4> for a slot of more than 64 events).
 __device__ __forceinline__ bool build_and_match(LsState& S) {
     const int EW = S.EW;
     // static indices into ts/mv_e/mv_t (unrolled to 3): a runtime index would
@@ -209,34 +306,61 @@ __device__ __forceinline__ bool build_and_match(LsState& S) {
         const LsTask T = get_task(S, k);
         const uint64_t* nb = S.NB + (size_t)k * EW;
         int N = 0;
-        bool over = false;
-        for (int w = 0; w < EW; ++w) {
-            uint64_t x = nb[w];
-            while (x) {
-                const int e = 64 * w + __builtin_ctzll(x);
-                x &= x - 1;
-                if (N < S.NT) { T.ev[N] = (uint16_t)e; T.pl[N] = S.pb.poss[e]; }
-                else over = true;
+        for (int w = 0; w < EW; ++w)
+            for (uint64_t x = nb[w]; x; x &= x - 1) {
+                if (N < S.NT) T.ev[N] = (uint16_t)(64 * w + __builtin_ctzll(x));
                 ++N;
             }
-        }
-        for (int r = 0; r < S.R; ++r) T.hist[r] = 0;
-        int pairs = 0;
-        if (over && S.NT < kMaxSlotEvents && S.NT < S.E) {
-            S.misc[3] = 1;                                          // first launch: redo with full tasks
-        } else if (over) {
-            atomicOr(S.pb.status, 1);
-            for (int i = 0; i < S.NT; ++i) S.nrr[T.ev[i]] = 0xFF;
-        } else if (N > 0) {
-            if (N <= 64) match_slot<1>(S.R, T.ev, T.pl, N, T.mr, T.rm, T.dr, S.nrr);
-            else match_slot<4>(S.R, T.ev, T.pl, N, T.mr, T.rm, T.dr, S.nrr);
-            for (int i = 0; i < N; ++i) {
-                const int r = S.nrr[T.ev[i]];
-                pairs += T.hist[r];
-                T.hist[r] = (uint16_t)(T.hist[r] + 1);
+        S.misc[4 + k] = N;
+    }
+    wave_sync();
+    // every task's events and possible rooms into registers at once (one L2 round trip)
+    int tn[3], tev[3];
+    uint64_t tpl[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        tn[k] = k < S.nts ? S.misc[4 + k] : 0;
+        const bool a = S.lane < tn[k] && tn[k] <= 64;
+        tev[k] = a ? get_task(S, k).ev[S.lane] : 0;
+        tpl[k] = a ? S.pb.poss[tev[k]] : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (k >= S.nts) break;
+        const int N = tn[k];
+        if (N > S.NT) {                                             // task capacity exceeded
+            if (S.lane == 0) {
+                if (S.NT < kMaxSlotEvents && S.NT < S.E) {
+                    S.misc[3] = 1;                                  // first launch: redo with full tasks
+                } else {
+                    atomicOr(S.pb.status, 1);
+                    const LsTask T = get_task(S, k);
+                    for (int i = 0; i < S.NT; ++i) S.nrr[T.ev[i]] = 0xFF;
+                    S.misc[k] = 0;
+                }
             }
+            wave_sync();
+            if (S.misc[3]) break;
+        } else if (N == 0) {
+            if (S.lane == 0) S.misc[k] = 0;
+        } else if (N <= 64) {
+            match_task_wave(S, k, N, tev[k], tpl[k]);
+        } else {                                                    // 64 < N <= 256: lane-serial matcher
+            if (S.lane == 0) {
+                const LsTask T = get_task(S, k);
+                for (int i = 0; i < N; ++i) T.pl[i] = S.pb.poss[T.ev[i]];
+                for (int r = 0; r < S.R; ++r) T.hist[r] = 0;
+                match_slot<4>(S.R, T.ev, T.pl, N, T.mr, T.rm, T.dr, S.nrr);
+                int pairs = 0;
+                for (int i = 0; i < N; ++i) {
+                    const int r = S.nrr[T.ev[i]];
+                    pairs += T.hist[r];
+                    T.hist[r] = (uint16_t)(T.hist[r] + 1);
+                }
+                S.misc[k] = pairs;
+            }
+            wave_sync();
         }
-        S.misc[k] = pairs;
     }
     wave_sync();
     return S.misc[3] != 0;
@@ -343,6 +467,7 @@ __global__ __launch_bounds__(64) void local_search_kernel(DevProblem pb, uint8_t
     S.B = (uint64_t*)(lds + L.B); S.NB = (uint64_t*)(lds + L.NB);
     S.rp = (int32_t*)(lds + L.rp); S.hist = (uint16_t*)(lds + L.hist);
     S.misc = (int32_t*)(lds + L.misc);
+    S.cnt = (uint32_t*)(lds + L.cnt);
     S.task_base = lds + L.task;
     S.task_bytes = (int)L.task_bytes;
     S.NT = L.NT;
