@@ -30,6 +30,20 @@ constexpr int kLsTasks = 3;
 // input by the second launch with tasks sized for kMaxSlotEvents.
 constexpr int kLsCapSmall = 64;
 
+// Profiling build (-DTT_LS_PROF, `make libttga_prof.so`, tools/ls_prof.py):
+// per-section shader-clock totals of every wave, summed into g_ls_prof.
+#ifdef TT_LS_PROF
+enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfN };
+__device__ unsigned long long g_ls_prof[kPfN];
+#define LSP_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define LSP_ADD(St, i, v) ((St).prof[i] += __builtin_amdgcn_s_memtime() - (v))
+#define LSP_CNT(St, i) ((St).prof[i] += 1)
+#else
+#define LSP_T(v)
+#define LSP_ADD(St, i, v)
+#define LSP_CNT(St, i)
+#endif
+
 struct LsLayout {
     size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, cnt, task;
     size_t task_bytes;
@@ -87,6 +101,13 @@ struct LsState {
     // neighbour description (wave-uniform)
     int nmv, mv_e[3], mv_t[3];
     int nts, ts[3];
+    // Move1 loops: the old slot minus the moved event (task 1) is the same set
+    // for every target slot, so its matching is kept from one rejected trial
+    // to the next (c1_valid) instead of being recomputed
+    int c1_valid;
+#ifdef TT_LS_PROF
+    uint64_t prof[kPfN];
+#endif
 };
 
 __device__ __forceinline__ LsTask get_task(const LsState& S, int k) {
@@ -116,16 +137,18 @@ __device__ __forceinline__ int slot_nb(const LsState& S, int j) {
 }
 
 // sum over words of popcount(corr64[e] & set[w]) - corr(e,e)  (the "i != e" of the reference)
-__device__ __forceinline__ int corr_in_set(const LsState& S, int e, const uint64_t* set) {
+__device__ __forceinline__ int corr_in_set(LsState& S, int e, const uint64_t* set) {
+    LSP_T(t0);
     int c = 0;
     for (int w = S.lane; w < S.EW; w += 64) c += __popcll(S.pb.corr64[(size_t)e * S.EW + w] & set[w]);
     c = wave_sum(c);
     const int self = (int)((S.pb.corr64[(size_t)e * S.EW + (e >> 6)] >> (e & 63)) & 1ull);
+    LSP_ADD(S, kPfCorr, t0);
     return c - self;
 }
 
 // eventAffectedHcv(e) (Solution.cpp:194-215) in the current state
-__device__ __forceinline__ int eah_cur(const LsState& S, int e) {
+__device__ __forceinline__ int eah_cur(LsState& S, int e) {
     const int t = S.sl[e];
     return S.rp[t] + corr_in_set(S, e, S.B + (size_t)t * S.EW);
 }
@@ -139,20 +162,21 @@ __device__ __forceinline__ int task_of(const LsState& S, int t) {
 }
 
 // eventAffectedHcv(e) in the neighbour
-__device__ __forceinline__ int eah_nb(const LsState& S, int e) {
+__device__ __forceinline__ int eah_nb(LsState& S, int e) {
     const int k = task_of(S, slot_nb(S, e));
     return S.misc[k] + corr_in_set(S, e, S.NB + (size_t)k * S.EW);
 }
 
 // eventHcv(e) (Solution.cpp:173-191) in the current state
-__device__ __forceinline__ int ehcv_cur(const LsState& S, int e) {
+__device__ __forceinline__ int ehcv_cur(LsState& S, int e) {
     const int t = S.sl[e];
     return (int)S.hist[t * S.R + S.rr[e]] - 1 + corr_in_set(S, e, S.B + (size_t)t * S.EW);
 }
 
 // eventScv(e) and singleClassesScv(e) (Solution.cpp:248-355) in the current
 // (nb = false) or neighbour (nb = true) state.
-__device__ __forceinline__ void scv_terms(const LsState& S, int e, bool nb, int& es, int& scs) {
+__device__ __forceinline__ void scv_terms(LsState& S, int e, bool nb, int& es, int& scs) {
+    LSP_T(t0);
     const DevProblem& pb = S.pb;
     const int t = nb ? slot_nb(S, e) : S.sl[e];
     const int day = t / 9, pos = t - 9 * day;
@@ -179,6 +203,7 @@ __device__ __forceinline__ void scv_terms(const LsState& S, int e, bool nb, int&
     }
     es = wave_sum(a) + (pos == 8 ? pb.sn[e] : 0);
     scs = wave_sum(b);
+    LSP_ADD(S, kPfScv, t0);
 }
 
 // Wave matcher for one touched slot of N <= 64 events, the same search as
@@ -193,6 +218,7 @@ __device__ __forceinline__ void scv_terms(const LsState& S, int e, bool nb, int&
 // room stage (ascending rooms, a matched room's event expanded at once) walks
 // step by step.
 __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev, uint64_t pl) {
+    LSP_T(t0);
     const int lane = S.lane, R = S.R;
     constexpr uint32_t NONE = 0xFFu;
     const bool act = lane < N;
@@ -272,12 +298,15 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
     if (lane < R) T.hist[lane] = (uint16_t)S.cnt[lane];
     pr = wave_sum(pr);
     if (lane == 0) S.misc[k] = pr;
+    LSP_ADD(S, kPfMatch, t0);
 }
 
 // Builds NB[k] for the touched slots and re-matches them: lane k lists the
 // events of slot k, then the wave matcher runs the slots one after another
 // (the lane-serial match_slot<4> for a slot of more than 64 events).
 __device__ __forceinline__ bool build_and_match(LsState& S) {
+    LSP_T(t0);
+    LSP_CNT(S, kPfTrials);
     const int EW = S.EW;
     // static indices into ts/mv_e/mv_t (unrolled to 3): a runtime index would
     // force the whole LsState into scratch and every LDS pointer through flat loads
@@ -327,6 +356,7 @@ __device__ __forceinline__ bool build_and_match(LsState& S) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         if (k >= S.nts) break;
+        if (k == 1 && S.c1_valid && S.nts == 2) continue;     // only set inside a Move1 loop
         const int N = tn[k];
         if (N > S.NT) {                                             // task capacity exceeded
             if (S.lane == 0) {
@@ -363,11 +393,13 @@ __device__ __forceinline__ bool build_and_match(LsState& S) {
         }
     }
     wave_sync();
+    LSP_ADD(S, kPfBuild, t0);
     return S.misc[3] != 0;
 }
 
 // events of neighbour slot k: copy rooms between rr and nrr
 __device__ __forceinline__ void sync_rooms(LsState& S, bool accept) {
+    LSP_T(t0);
     for (int k = 0; k < S.nts; ++k) {
         const uint64_t* nb = S.NB + (size_t)k * S.EW;
         for (int w = S.lane; w < S.EW; w += 64) {
@@ -381,9 +413,45 @@ __device__ __forceinline__ void sync_rooms(LsState& S, bool accept) {
         }
     }
     wave_sync();
+    LSP_ADD(S, kPfSync, t0);
+}
+
+// nrr = rr for the events of neighbour slot K
+template <int K>
+__device__ __forceinline__ void restore_task(LsState& S) {
+    const uint64_t* nb = S.NB + (size_t)K * S.EW;
+    for (int w = S.lane; w < S.EW; w += 64)
+        for (uint64_t x = nb[w]; x; x &= x - 1) {
+            const int e = 64 * w + __builtin_ctzll(x);
+            S.nrr[e] = S.rr[e];
+        }
+    wave_sync();
+}
+
+// Rejected Move1 trial. A two-slot neighbour (target t, then the old slot)
+// keeps task 1 -- the old slot minus the moved event, the same set for every
+// target -- matched in nrr, NB[1], hist and misc[1] for the next trial.
+__device__ __forceinline__ void reject_move1(LsState& S) {
+    if (S.nts == 2) {
+        restore_task<0>(S);
+        S.c1_valid = 1;
+    } else {                          // t == old slot: everything re-matched, drop the kept task
+        sync_rooms(S, false);
+        S.c1_valid = 0;
+    }
+}
+
+// end of a Move1 loop: restore the kept task
+__device__ __forceinline__ void cache_drop(LsState& S) {
+    if (S.c1_valid) {
+        restore_task<1>(S);
+        S.c1_valid = 0;
+    }
 }
 
 __device__ __forceinline__ void accept(LsState& S) {
+    LSP_T(t0);
+    S.c1_valid = 0;
     sync_rooms(S, true);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -402,6 +470,7 @@ __device__ __forceinline__ void accept(LsState& S) {
             if (q < S.nmv) S.sl[S.mv_e[q]] = (uint8_t)S.mv_t[q];
     }
     wave_sync();
+    LSP_ADD(S, kPfSync, t0);
 }
 
 __device__ __forceinline__ void add_touched(LsState& S, int t) {
@@ -431,7 +500,8 @@ __device__ __forceinline__ void set_move(LsState& S, int type, int e1, int a2, i
 }
 
 // whole-solution feasibility (Solution.cpp:63-84) from the incremental state
-__device__ __forceinline__ bool feasible_now(const LsState& S) {
+__device__ __forceinline__ bool feasible_now(LsState& S) {
+    LSP_T(t0);
     int h = 0;
     for (int t = S.lane; t < kSlots; t += 64) h += S.rp[t];
     for (int e = S.lane; e < S.E; e += 64) {
@@ -442,7 +512,9 @@ __device__ __forceinline__ bool feasible_now(const LsState& S) {
         h += c;   // every correlated same-slot pair is counted twice, only zero matters
         h += (int)(((S.pb.poss[e] >> S.rr[e]) & 1ull) ^ 1ull);
     }
-    return wave_sum(h) == 0;
+    const bool f = wave_sum(h) == 0;
+    LSP_ADD(S, kPfFeas, t0);
+    return f;
 }
 
 // CAP = matcher task capacity. redo_out (first launch): set to 1 for an
@@ -459,6 +531,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
     const int lane = threadIdx.x;
     const long p = blockIdx.x;
     if (redo_in && !redo_in[p]) return;
+    LSP_T(t_kernel);
     const LsLayout L = ls_layout(E, R, EW, CAP);
     LsState S;
     S.pb = pb; S.E = E; S.R = R; S.EW = EW; S.lane = lane;
@@ -472,6 +545,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
     S.task_bytes = (int)L.task_bytes;
     S.NT = L.NT;
     S.nmv = 0; S.nts = 0;
+    S.c1_valid = 0;
+#ifdef TT_LS_PROF
+#pragma unroll
+    for (int i = 0; i < kPfN; ++i) S.prof[i] = 0;
+#endif
     if (lane == 0) S.misc[3] = 0;
 
     // ---- load the individual, derive the incremental state
@@ -524,6 +602,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
     for (int i = 0; i < E; ++i) pm_next(st);    // every lane keeps the (uniform) stream
     __syncthreads();
 
+    LSP_ADD(S, kPfInit, t_kernel);
     int step = 0, evc = 0;
     bool better = false;
     const long guard_max = 4l * (long)E * ((long)max_steps + 2) + 1024;
@@ -532,6 +611,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
         for (int i = 0; evc < E; i = (i + 1) % E) {
             if (step > max_steps || ++guard > guard_max) break;
             const int ei = S.evl[i];
+            LSP_CNT(S, kPfVisits);
             if (ehcv_cur(S, ei) == 0) { evc++; continue; }
             const int t_start = pm_pick(st, kSlots);
             const int t_orig = S.sl[ei];
@@ -544,9 +624,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                     const int n = eah_nb(S, ei) + S.misc[task_of(S, t_orig)];
                     const int c = eah_cur(S, ei) + S.rp[t];
                     if (n < c) { accept(S); evc = 0; better = true; break; }
-                    sync_rooms(S, false);
+                    reject_move1(S);
                 }
             }
+            cache_drop(S);
             if (better) { better = false; continue; }
             if (p2 != 0) {
                 for (int j = (i + 1) % E; j != i; j = (j + 1) % E) {
@@ -602,6 +683,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
         for (int i = 0; evc < E; i = (i + 1) % E) {
             if (step > max_steps || ++guard > guard_max) break;
             const int ei = S.evl[i];
+            LSP_CNT(S, kPfVisits);
             int cur, scs_i;
             scv_terms(S, ei, false, cur, scs_i);
             if (cur == 0) { evc++; continue; }
@@ -617,9 +699,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         scv_terms(S, ei, true, es_n, scs_n);
                         if (es_n + scs_i - scs_n < cur) { accept(S); evc = 0; better = true; break; }
                     }
-                    sync_rooms(S, false);
+                    reject_move1(S);
                 }
             }
+            cache_drop(S);
             if (better) { better = false; continue; }
             if (p2 != 0) {
                 for (int j = (i + 1) % E; j != i; j = (j + 1) % E) {
@@ -684,6 +767,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
         room[p * E + e] = S.rr[e];
     }
     if (lane == 0) rng[p] = st;
+#ifdef TT_LS_PROF
+    LSP_ADD(S, kPfTotal, t_kernel);
+    LSP_CNT(S, kPfWaves);
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < kPfN; ++i) atomicAdd(&g_ls_prof[i], (unsigned long long)S.prof[i]);
+    }
+#endif
     return;
 redo:
     if (lane == 0) redo_out[p] = 1;
@@ -692,6 +783,18 @@ redo:
 }  // namespace ttga
 
 using namespace ttga;
+
+#ifdef TT_LS_PROF
+extern "C" int tt_ls_prof_read(unsigned long long* out, int reset) {
+    TT_HIP(hipDeviceSynchronize());
+    TT_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ls_prof), sizeof(unsigned long long) * kPfN));
+    if (reset) {
+        unsigned long long z[kPfN] = {};
+        TT_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ls_prof), z, sizeof(z)));
+    }
+    return kPfN;
+}
+#endif
 
 extern "C" int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P,
                                int max_steps, double p1, double p2, double p3, void* stream) {

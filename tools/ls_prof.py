@@ -1,0 +1,51 @@
+"""Section profile of the local-search kernel (profiling build libttga_prof.so,
+-DTT_LS_PROF): shader-clock totals over all waves of one batch, per trial and
+per wave. Same workload as tools/bench_ls.py (med, pop 4096, maxSteps 200 from
+RandomInitialSolution)."""
+import argparse
+import ctypes
+import json
+import pathlib
+import sys
+
+REPO = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "timetabling-ga-mpi-openmp_amd"))
+import torch  # noqa: E402
+
+import ttga  # noqa: E402
+from ttga import native  # noqa: E402
+
+NAMES = ["init", "build_and_match", "match_task_wave", "corr_in_set", "scv_terms", "sync_accept", "feasible_now",
+         "total", "trials", "event_visits", "waves"]
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="med")
+ap.add_argument("--pop", type=int, default=4096)
+ap.add_argument("--steps", type=int, default=200)
+a = ap.parse_args()
+
+lib = native.load(native.PKG_DIR / "libttga_prof.so")
+native._lib = lib
+lib.tt_ls_prof_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+lib.tt_ls_prof_read.restype = ctypes.c_int
+inst = ttga.config_instance(a.config)
+dp = native.DeviceProblem(inst)
+P, E = a.pop, inst.E
+s = torch.empty((P, E), dtype=torch.uint8, device="cuda")
+r = torch.empty_like(s)
+dp.random_init(torch.from_numpy(ttga.population_seeds(1000, P)).cuda(), s, r)
+g = torch.from_numpy(ttga.population_seeds(9000, P)).cuda()
+buf = (ctypes.c_ulonglong * 16)()
+lib.tt_ls_prof_read(buf, 1)
+dp.local_search(s, r, g, a.steps)
+torch.cuda.synchronize()
+n = lib.tt_ls_prof_read(buf, 1)
+v = {NAMES[i]: int(buf[i]) for i in range(n)}
+trials, waves = max(v["trials"], 1), max(v["waves"], 1)
+out = {"config": a.config, "pop": P, "max_steps": a.steps, "raw": v,
+       "cycles_per_trial": {k: v[k] / trials for k in NAMES[:7]},
+       "cycles_per_wave": {k: v[k] / waves for k in NAMES[:8]},
+       "trials_per_wave": v["trials"] / waves, "visits_per_wave": v["event_visits"] / waves,
+       "note": "s_memtime deltas summed over waves that finished in the first launch; sections nest "
+               "(match_task_wave and corr_in_set inside build_and_match/deltas)"}
+print(json.dumps(out, indent=1))
