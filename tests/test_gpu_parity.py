@@ -278,3 +278,27 @@ def test_local_search_crowded_slots_redo(orc):
     es, er, eg = o.local_search(s0, r0, seeds, 300)
     assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg)
     assert dp.status() == 0
+
+
+@pytest.mark.parametrize("p1,p2", [(1.0, 1.0), (0.7, 0.4)])
+def test_local_search_phase2_vs_oracle(orc, p1, p2):
+    """Mostly-feasible individuals (3000 steps from random init), then a chained
+    run that starts in phase 2 (Solution.cpp:619-768): the lazy matching of the
+    trial neighbours (exact lower-bound rejection before the target slot is
+    matched, the old slot matched only for an accepted Move1) must keep slots,
+    rooms and RNG states identical to the oracle."""
+    inst = ttga.generate(300, 12, 4, 150, seed=31)
+    dp = native.DeviceProblem(inst)
+    o = orc.problem(inst)
+    P = 32
+    s0, r0, _ = o.random_init(ttga.population_seeds(1201, P))
+    seeds = ttga.population_seeds(1301, P)
+    s, r, g = dev(s0), dev(r0), dev(seeds)
+    dp.local_search(s, r, g, 3000, p1, p2)
+    es, er, eg = o.local_search(s0, r0, seeds, 3000, p1, p2)
+    assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg)
+    assert int(o.eval(es, er)[2].sum()) >= P // 2          # phase 2 is exercised below
+    dp.local_search(s, r, g, 2000, p1, p2)
+    es, er, eg = o.local_search(es, er, eg, 2000, p1, p2)
+    assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg)
+    assert dp.status() == 0

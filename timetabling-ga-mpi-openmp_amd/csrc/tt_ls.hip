@@ -167,6 +167,11 @@ __device__ __forceinline__ int eah_nb(LsState& S, int e) {
     return S.misc[k] + corr_in_set(S, e, S.NB + (size_t)k * S.EW);
 }
 
+// the correlation part of eventAffectedHcv(e) in the neighbour (needs NB, not rooms)
+__device__ __forceinline__ int corr_nb(LsState& S, int e) {
+    return corr_in_set(S, e, S.NB + (size_t)task_of(S, slot_nb(S, e)) * S.EW);
+}
+
 // eventHcv(e) (Solution.cpp:173-191) in the current state
 __device__ __forceinline__ int ehcv_cur(LsState& S, int e) {
     const int t = S.sl[e];
@@ -224,34 +229,38 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
     const bool act = lane < N;
     const uint32_t pl_lo = (uint32_t)pl, pl_hi = (uint32_t)(pl >> 32);
     // transpose: ev_of_room (lane j) = the events whose possible rooms include j
+    // (8 independent ballots per block; pl has no bits at or above R)
     uint64_t eor = 0;
-    for (int j = 0; j < R; ++j) {
-        const uint64_t b = __ballot(act && ((pl >> j) & 1ull));
-        if (lane == j) eor = b;
+    for (int j0 = 0; j0 < R; j0 += 8) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t b = __ballot(act && ((pl >> (j0 + q)) & 1ull));
+            if (lane == j0 + q) eor = b;
+        }
     }
-    uint32_t mr = NONE, rm = 0, dr = 0;
+    // lane j also keeps the possible rooms of its matched event (plr), so a
+    // search step reads rm and plr at the same lane j: no dependent readlane
+    uint32_t mr = NONE, rm = 0, dr = 0, plr_lo = 0, plr_hi = 0;
     uint64_t unm = N >= 64 ? ~0ull : ((1ull << N) - 1ull);
     uint64_t rmatched = 0;
     for (;;) {
         // stage 1 (closed form): expand all unmatched events, ascending
         const uint64_t cand = eor & unm;
-        uint64_t sr = __ballot(lane < R && cand != 0ull), fr = sr, se = unm;
+        uint64_t sr = __ballot(lane < R && cand != 0ull), fr = sr;
         if (cand) dr = (uint32_t)__builtin_ctzll(cand);
-        // stage 2: fringe rooms ascending; a matched room's event is expanded at once
+        // stage 2: fringe rooms ascending; a matched room's event is expanded at
+        // once. Each room enters the fringe once and each matched event is
+        // reached only through its own room (already seen), so neither a seen-
+        // event test nor the event's own room needs masking.
         int sink = -1;
         while (fr) {
             const int j = __builtin_ctzll(fr);
             fr &= fr - 1;
             if (!((rmatched >> j) & 1ull)) { sink = j; break; }     // free room: the path is fixed
             const int i2 = __builtin_amdgcn_readlane((int)rm, j);
-            const uint64_t bi = 1ull << i2;
-            if (se & bi) continue;
-            se |= bi;
-            const uint32_t mi = (uint32_t)__builtin_amdgcn_readlane((int)mr, i2);
-            const uint64_t own = mi != NONE ? (1ull << mi) : 0ull;
-            const uint64_t pli = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)pl_hi, i2) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readlane((int)pl_lo, i2);
-            const uint64_t nr = pli & ~sr & ~own;
+            const uint64_t pli = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)plr_hi, j) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)plr_lo, j);
+            const uint64_t nr = pli & ~sr;
             sr |= nr;
             fr |= nr;
             if ((nr >> lane) & 1ull) dr = (uint32_t)i2;
@@ -262,8 +271,10 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
         for (;;) {
             const int i = __builtin_amdgcn_readlane((int)dr, j);
             const uint32_t prev = (uint32_t)__builtin_amdgcn_readlane((int)mr, i);
+            const uint32_t pi_lo = (uint32_t)__builtin_amdgcn_readlane((int)pl_lo, i);
+            const uint32_t pi_hi = (uint32_t)__builtin_amdgcn_readlane((int)pl_hi, i);
             if (lane == i) mr = (uint32_t)j;
-            if (lane == j) rm = (uint32_t)i;
+            if (lane == j) { rm = (uint32_t)i; plr_lo = pi_lo; plr_hi = pi_hi; }
             rmatched |= 1ull << j;
             if (prev == NONE) { unm &= ~(1ull << i); break; }
             j = (int)prev;
@@ -286,25 +297,27 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
     const int src = below ? 63 - __builtin_clzll(below) : lane;
     const uint32_t carried = (uint32_t)__shfl((int)v, src, 64);
     const uint32_t r = !un ? mr : (pl ? v : (below ? carried : 0u));
+    // room histogram (lane j = room j) and the pairs of events sharing a room,
+    // from one ballot per room (r < R for every event)
     const LsTask T = get_task(S, k);
-    if (lane < R) S.cnt[lane] = 0u;
-    wave_sync();
+    uint32_t cnt_r = 0;
     int pr = 0;
-    if (act) {
-        S.nrr[ev] = (uint8_t)r;
-        pr = (int)atomicAdd(&S.cnt[r], 1u);            // pairs of events sharing a room
+    for (int j0 = 0; j0 < R; j0 += 8) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int c = __popcll(__ballot(act && r == (uint32_t)(j0 + q)));
+            pr += c * (c - 1) / 2;
+            if (lane == j0 + q) cnt_r = (uint32_t)c;
+        }
     }
-    wave_sync();
-    if (lane < R) T.hist[lane] = (uint16_t)S.cnt[lane];
-    pr = wave_sum(pr);
+    if (act) S.nrr[ev] = (uint8_t)r;
+    if (lane < R) T.hist[lane] = (uint16_t)cnt_r;
     if (lane == 0) S.misc[k] = pr;
     LSP_ADD(S, kPfMatch, t0);
 }
 
-// Builds NB[k] for the touched slots and re-matches them: lane k lists the
-// events of slot k, then the wave matcher runs the slots one after another
-// (the lane-serial match_slot<4> for a slot of more than 64 events).
-__device__ __forceinline__ bool build_and_match(LsState& S) {
+// Builds NB[k] for the touched slots; lane k lists the events of slot k.
+__device__ __forceinline__ void build_nb(LsState& S) {
     LSP_T(t0);
     LSP_CNT(S, kPfTrials);
     const int EW = S.EW;
@@ -343,12 +356,20 @@ __device__ __forceinline__ bool build_and_match(LsState& S) {
         S.misc[4 + k] = N;
     }
     wave_sync();
+    LSP_ADD(S, kPfBuild, t0);
+}
+
+// Re-matches the touched slots in kmask (after build_nb): the wave matcher runs
+// the slots one after another (the lane-serial match_slot<4> for a slot of more
+// than 64 events). Returns true when the first launch must redo the individual.
+__device__ __forceinline__ bool match_tasks(LsState& S, int kmask) {
+    LSP_T(t0);
     // every task's events and possible rooms into registers at once (one L2 round trip)
     int tn[3], tev[3];
     uint64_t tpl[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        tn[k] = k < S.nts ? S.misc[4 + k] : 0;
+        tn[k] = k < S.nts && ((kmask >> k) & 1) ? S.misc[4 + k] : 0;
         const bool a = S.lane < tn[k] && tn[k] <= 64;
         tev[k] = a ? get_task(S, k).ev[S.lane] : 0;
         tpl[k] = a ? S.pb.poss[tev[k]] : 0ull;
@@ -356,7 +377,8 @@ __device__ __forceinline__ bool build_and_match(LsState& S) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         if (k >= S.nts) break;
-        if (k == 1 && S.c1_valid && S.nts == 2) continue;     // only set inside a Move1 loop
+        if (!((kmask >> k) & 1)) continue;
+        if (k == 1 && S.c1_valid && S.nts == 2) continue;     // only set inside a phase-1 Move1 loop
         const int N = tn[k];
         if (N > S.NT) {                                             // task capacity exceeded
             if (S.lane == 0) {
@@ -395,6 +417,11 @@ __device__ __forceinline__ bool build_and_match(LsState& S) {
     wave_sync();
     LSP_ADD(S, kPfBuild, t0);
     return S.misc[3] != 0;
+}
+
+__device__ __forceinline__ bool build_and_match(LsState& S) {
+    build_nb(S);
+    return match_tasks(S, 7);
 }
 
 // events of neighbour slot k: copy rooms between rr and nrr
@@ -620,10 +647,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                 if (pm_next(st) < p1) {
                     step++;
                     set_move(S, 1, ei, t, 0);
-                    if (build_and_match(S)) goto redo;
-                    const int n = eah_nb(S, ei) + S.misc[task_of(S, t_orig)];
+                    build_nb(S);
                     const int c = eah_cur(S, ei) + S.rp[t];
-                    if (n < c) { accept(S); evc = 0; better = true; break; }
+                    if (S.nts == 2) {
+                        // task 0 = t plus ei, task 1 = t_orig minus ei (kept across trials).
+                        // n = corr + misc[1] + misc[0] >= corr + misc[1]: a trial that cannot
+                        // win is rejected before the target slot is matched.
+                        if (match_tasks(S, 2)) goto redo;
+                        const int lb = corr_nb(S, ei) + S.misc[1];
+                        if (lb >= c) { S.c1_valid = 1; continue; }
+                        if (match_tasks(S, 1)) goto redo;
+                        if (lb + S.misc[0] < c) { accept(S); evc = 0; better = true; break; }
+                    } else {
+                        if (match_tasks(S, 7)) goto redo;
+                        const int n = eah_nb(S, ei) + S.misc[task_of(S, t_orig)];
+                        if (n < c) { accept(S); evc = 0; better = true; break; }
+                    }
                     reject_move1(S);
                 }
             }
@@ -637,8 +676,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         const int ej = S.evl[j];
                         const int c = eah_cur(S, ei) + eah_cur(S, ej);
                         set_move(S, 2, ei, ej, 0);
-                        if (build_and_match(S)) goto redo;
-                        const int n = eah_nb(S, ei) + eah_nb(S, ej);
+                        build_nb(S);
+                        const int lb = corr_nb(S, ei) + corr_nb(S, ej);    // n >= lb whatever the rooms
+                        if (lb >= c) continue;
+                        if (match_tasks(S, 7)) goto redo;
+                        const int n = lb + S.misc[task_of(S, slot_nb(S, ei))] + S.misc[task_of(S, slot_nb(S, ej))];
                         if (n < c) { accept(S); evc = 0; better = true; break; }
                         sync_rooms(S, false);
                     }
@@ -693,13 +735,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                 if (pm_next(st) < p1) {
                     step++;
                     set_move(S, 1, ei, t, 0);
-                    if (build_and_match(S)) goto redo;
-                    if (eah_nb(S, ei) == 0) {
+                    build_nb(S);
+                    // eah_nb(ei) == 0 needs no correlated event in t (no rooms needed)
+                    // and no room clash in t (task 0); the old slot (task 1) is
+                    // matched only for an accepted move
+                    if (corr_nb(S, ei) != 0) continue;
+                    if (match_tasks(S, 1)) goto redo;
+                    if (S.misc[0] == 0) {
                         int es_n, scs_n;
                         scv_terms(S, ei, true, es_n, scs_n);
-                        if (es_n + scs_i - scs_n < cur) { accept(S); evc = 0; better = true; break; }
+                        if (es_n + scs_i - scs_n < cur) {
+                            if (match_tasks(S, 2)) goto redo;
+                            accept(S); evc = 0; better = true; break;
+                        }
                     }
-                    reject_move1(S);
+                    restore_task<0>(S);
                 }
             }
             cache_drop(S);
@@ -711,8 +761,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         step++;
                         const int ej = S.evl[j];
                         set_move(S, 2, ei, ej, 0);
-                        if (build_and_match(S)) goto redo;
-                        if (eah_nb(S, ei) + eah_nb(S, ej) == 0) {
+                        build_nb(S);
+                        if (corr_nb(S, ei) + corr_nb(S, ej) != 0) continue;   // eah_nb > 0 whatever the rooms
+                        if (match_tasks(S, 7)) goto redo;
+                        if (S.misc[task_of(S, slot_nb(S, ei))] + S.misc[task_of(S, slot_nb(S, ej))] == 0) {
                             int es_ni, scs_ni, es_nj, scs_nj, es_cj, scs_cj;
                             scv_terms(S, ei, true, es_ni, scs_ni);
                             scv_terms(S, ej, true, es_nj, scs_nj);
