@@ -40,7 +40,7 @@ KERNELS = {1: "eval_tile", 2: "eval_block", 3: "eval_tile4", 4: "eval_tile4_w8",
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--pop", type=int, default=POP_PER_GPU)
     ap.add_argument("--config", default="med", choices=["sm", "med", "lg", "syn"])

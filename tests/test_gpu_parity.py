@@ -302,3 +302,27 @@ def test_local_search_phase2_vs_oracle(orc, p1, p2):
     es, er, eg = o.local_search(es, er, eg, 2000, p1, p2)
     assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg)
     assert dp.status() == 0
+
+
+def test_rng_edge_seeds_vs_oracle(orc):
+    """Park-Miller states outside [0, 2^31 - 1) take the 64-bit Schrage path on
+    their first draw (Random.cc:27-37; every later state is in range and takes
+    the 32-bit path): zero, negative, 2^31 and beyond, through random init and
+    local search, against the oracle."""
+    inst = ttga.generate(120, 6, 4, 90, seed=41)
+    dp = native.DeviceProblem(inst)
+    o = orc.problem(inst)
+    # (seeds whose first draw leaves [0, 2^31 - 1), e.g. 2^40, give the reference
+    # negative or >= 1 draws and out-of-range slots: undefined there, not tested)
+    seeds = np.array([0, 1, -1, -123456789, -2_000_000_000, 2**31 - 2, 2**31 - 1, 2**31, 2**31 + 5,
+                      3_000_000_000, 4_000_000_000, 42], dtype=np.int64)
+    es, er, eg = o.random_init(seeds.copy())
+    s = torch.empty((seeds.size, inst.E), dtype=torch.uint8, device="cuda")
+    r = torch.empty_like(s)
+    g = dev(seeds.copy())
+    dp.random_init(g, s, r)
+    assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg)
+    g = dev(seeds.copy())
+    dp.local_search(s, r, g, 300)
+    ls, lr, lg = o.local_search(es, er, seeds.copy(), 300)
+    assert np.array_equal(host(s), ls) and np.array_equal(host(r), lr) and np.array_equal(host(g), lg)

@@ -50,9 +50,20 @@ __host__ __device__ constexpr int sch_part_base(int nw) { return nw == 4 ? kSchP
 // Park-Miller "minimal standard" generator, Schrage's method
 // (Random.h:15-19, Random.cc:27-37). Bit-exact with the reference: int64
 // state arithmetic, then AM * state in IEEE fp64 (gfx950 has full fp64).
+// Every state after the first draw lies in [0, 2^31 - 1), where Schrage's
+// steps fit 32-bit integers exactly (16807 * 127772 < 2^31 - 1), so the
+// 64-bit form is only needed for an out-of-range initial seed.
 __device__ __forceinline__ double pm_next(int64_t& s) {
     const int64_t IA = 16807, IM = 2147483647, IQ = 127773, IR = 2836;
     const double AM = 1.0 / 2147483647.0;
+    if ((uint64_t)s <= 0x7FFFFFFFull) {
+        const uint32_t u = (uint32_t)s;
+        const uint32_t k32 = u / 127773u;
+        int32_t t = 16807 * (int32_t)(u - k32 * 127773u) - 2836 * (int32_t)k32;
+        if (t < 0) t += 2147483647;
+        s = t;
+        return __dmul_rn(AM, (double)t);
+    }
     int64_t k = s / IQ;
     s = IA * (s - k * IQ) - IR * k;
     if (s < 0) s += IM;

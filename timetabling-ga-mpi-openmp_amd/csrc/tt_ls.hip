@@ -33,7 +33,7 @@ constexpr int kLsCapSmall = 64;
 // Profiling build (-DTT_LS_PROF, `make libttga_prof.so`, tools/ls_prof.py):
 // per-section shader-clock totals of every wave, summed into g_ls_prof.
 #ifdef TT_LS_PROF
-enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfN };
+enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfN };
 __device__ unsigned long long g_ls_prof[kPfN];
 #define LSP_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define LSP_ADD(St, i, v) ((St).prof[i] += __builtin_amdgcn_s_memtime() - (v))
@@ -615,19 +615,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
     }
     __syncthreads();
 
+    LSP_T(t_scr);
     int64_t st = rng[p];
-    // scramble the event list (Solution.cpp:476-484)
-    if (lane == 0) {
-        int64_t s2 = st;
-        for (int i = 0; i < E; ++i) {
-            const int j = pm_pick(s2, E);
+    // scramble the event list (Solution.cpp:476-484): the stream is wave-uniform,
+    // lane 0 does the swaps, and the next draw overlaps the LDS round trip
+    for (int i = 0; i < E; ++i) {
+        const int j = pm_pick(st, E);
+        if (lane == 0) {
             const uint16_t h = S.evl[i];
             S.evl[i] = S.evl[j];
             S.evl[j] = h;
         }
     }
-    for (int i = 0; i < E; ++i) pm_next(st);    // every lane keeps the (uniform) stream
     __syncthreads();
+    LSP_ADD(S, kPfScramble, t_scr);
 
     LSP_ADD(S, kPfInit, t_kernel);
     int step = 0, evc = 0;
@@ -679,7 +680,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         build_nb(S);
                         const int lb = corr_nb(S, ei) + corr_nb(S, ej);    // n >= lb whatever the rooms
                         if (lb >= c) continue;
-                        if (match_tasks(S, 7)) goto redo;
+                        if (S.nts == 2) {             // task 0 = slot(ej) plus ei, task 1 = slot(ei) plus ej
+                            if (match_tasks(S, 1)) goto redo;
+                            if (lb + S.misc[0] >= c) { restore_task<0>(S); continue; }
+                            if (match_tasks(S, 2)) goto redo;
+                        } else if (match_tasks(S, 7)) goto redo;
                         const int n = lb + S.misc[task_of(S, slot_nb(S, ei))] + S.misc[task_of(S, slot_nb(S, ej))];
                         if (n < c) { accept(S); evc = 0; better = true; break; }
                         sync_rooms(S, false);
@@ -763,7 +768,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         set_move(S, 2, ei, ej, 0);
                         build_nb(S);
                         if (corr_nb(S, ei) + corr_nb(S, ej) != 0) continue;   // eah_nb > 0 whatever the rooms
-                        if (match_tasks(S, 7)) goto redo;
+                        if (S.nts == 2) {
+                            if (match_tasks(S, 1)) goto redo;
+                            if (S.misc[0] != 0) { restore_task<0>(S); continue; }
+                            if (match_tasks(S, 2)) goto redo;
+                        } else if (match_tasks(S, 7)) goto redo;
                         if (S.misc[task_of(S, slot_nb(S, ei))] + S.misc[task_of(S, slot_nb(S, ej))] == 0) {
                             int es_ni, scs_ni, es_nj, scs_nj, es_cj, scs_cj;
                             scv_terms(S, ei, true, es_ni, scs_ni);

@@ -16,7 +16,7 @@ import ttga  # noqa: E402
 from ttga import native  # noqa: E402
 
 NAMES = ["init", "build_and_match", "match_task_wave", "corr_in_set", "scv_terms", "sync_accept", "feasible_now",
-         "total", "trials", "event_visits", "waves"]
+         "total", "trials", "event_visits", "waves", "scramble"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="med")
@@ -44,7 +44,7 @@ v = {NAMES[i]: int(buf[i]) for i in range(n)}
 trials, waves = max(v["trials"], 1), max(v["waves"], 1)
 out = {"config": a.config, "pop": P, "max_steps": a.steps, "raw": v,
        "cycles_per_trial": {k: v[k] / trials for k in NAMES[:7]},
-       "cycles_per_wave": {k: v[k] / waves for k in NAMES[:8]},
+       "cycles_per_wave": {k: v[k] / waves for k in NAMES[:8] + ["scramble"]},
        "trials_per_wave": v["trials"] / waves, "visits_per_wave": v["event_visits"] / waves,
        "note": "s_memtime deltas summed over waves that finished in the first launch; sections nest "
                "(match_task_wave and corr_in_set inside build_and_match/deltas)"}
