@@ -33,7 +33,7 @@ constexpr int kLsCapSmall = 64;
 // Profiling build (-DTT_LS_PROF, `make libttga_prof.so`, tools/ls_prof.py):
 // per-section shader-clock totals of every wave, summed into g_ls_prof.
 #ifdef TT_LS_PROF
-enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfN };
+enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfN };
 __device__ unsigned long long g_ls_prof[kPfN];
 #define LSP_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define LSP_ADD(St, i, v) ((St).prof[i] += __builtin_amdgcn_s_memtime() - (v))
@@ -224,6 +224,10 @@ __device__ __forceinline__ void scv_terms(LsState& S, int e, bool nb, int& es, i
 // step by step.
 __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev, uint64_t pl) {
     LSP_T(t0);
+    LSP_CNT(S, kPfMatchCalls);
+#ifdef TT_LS_PROF
+    S.prof[kPfMatchEvents] += N;
+#endif
     const int lane = S.lane, R = S.R;
     constexpr uint32_t NONE = 0xFFu;
     const bool act = lane < N;
@@ -252,11 +256,24 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
         // once. Each room enters the fringe once and each matched event is
         // reached only through its own room (already seen), so neither a seen-
         // event test nor the event's own room needs masking.
+        // Bulk form of the ascending walk: every fringe room below the lowest
+        // free one is matched, and popping a room whose event reaches no unseen
+        // room changes nothing but the fringe, so all such rooms up to the first
+        // one that does discover rooms (one ballot over the room lanes) are
+        // popped at once; that room is expanded as in the step-by-step walk.
         int sink = -1;
-        while (fr) {
-            const int j = __builtin_ctzll(fr);
-            fr &= fr - 1;
-            if (!((rmatched >> j) & 1ull)) { sink = j; break; }     // free room: the path is fixed
+        for (;;) {
+            const uint64_t freef = fr & ~rmatched;
+            const uint64_t M = fr & (freef ? (freef & (0ull - freef)) - 1ull : ~0ull);
+            const uint64_t plr = ((uint64_t)plr_hi << 32) | plr_lo;
+            const uint64_t disc = __ballot(((M >> lane) & 1ull) && (plr & ~sr) != 0ull);
+            LSP_CNT(S, kPfMatchSteps);
+            if (!disc) {                                   // the walk reaches the lowest free room
+                if (freef) sink = __builtin_ctzll(freef);
+                break;
+            }
+            const int j = __builtin_ctzll(disc);
+            fr &= ~(M & ((2ull << j) - 1ull));             // pops M's rooms up to j (j <= 63)
             const int i2 = __builtin_amdgcn_readlane((int)rm, j);
             const uint64_t pli = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)plr_hi, j) << 32) |
                                  (uint32_t)__builtin_amdgcn_readlane((int)plr_lo, j);
@@ -363,6 +380,9 @@ __device__ __forceinline__ void build_nb(LsState& S) {
 // the slots one after another (the lane-serial match_slot<4> for a slot of more
 // than 64 events). Returns true when the first launch must redo the individual.
 __device__ __forceinline__ bool match_tasks(LsState& S, int kmask) {
+    // task 1 kept from the previous rejected Move1 trial (set only inside a phase-1 Move1 loop)
+    if (S.c1_valid && S.nts == 2) kmask &= ~2;
+    if (!(kmask & ((1 << S.nts) - 1))) return false;            // nothing to match: no loads, no sync
     LSP_T(t0);
     // every task's events and possible rooms into registers at once (one L2 round trip)
     int tn[3], tev[3];
@@ -378,7 +398,6 @@ __device__ __forceinline__ bool match_tasks(LsState& S, int kmask) {
     for (int k = 0; k < 3; ++k) {
         if (k >= S.nts) break;
         if (!((kmask >> k) & 1)) continue;
-        if (k == 1 && S.c1_valid && S.nts == 2) continue;     // only set inside a phase-1 Move1 loop
         const int N = tn[k];
         if (N > S.NT) {                                             // task capacity exceeded
             if (S.lane == 0) {

@@ -16,7 +16,7 @@ import ttga  # noqa: E402
 from ttga import native  # noqa: E402
 
 NAMES = ["init", "build_and_match", "match_task_wave", "corr_in_set", "scv_terms", "sync_accept", "feasible_now",
-         "total", "trials", "event_visits", "waves", "scramble"]
+         "total", "trials", "event_visits", "waves", "scramble", "match_calls", "match_events", "match_steps"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="med")
