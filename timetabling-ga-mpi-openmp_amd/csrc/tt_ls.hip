@@ -379,21 +379,34 @@ __device__ __forceinline__ void build_nb(LsState& S) {
 // Re-matches the touched slots in kmask (after build_nb): the wave matcher runs
 // the slots one after another (the lane-serial match_slot<4> for a slot of more
 // than 64 events). Returns true when the first launch must redo the individual.
-__device__ __forceinline__ bool match_tasks(LsState& S, int kmask) {
-    // task 1 kept from the previous rejected Move1 trial (set only inside a phase-1 Move1 loop)
-    if (S.c1_valid && S.nts == 2) kmask &= ~2;
-    if (!(kmask & ((1 << S.nts) - 1))) return false;            // nothing to match: no loads, no sync
-    LSP_T(t0);
-    // every task's events and possible rooms into registers at once (one L2 round trip)
+struct TaskRegs {
     int tn[3], tev[3];
     uint64_t tpl[3];
+};
+
+// every task's events and possible rooms into registers at once (one L2 round
+// trip), issued as early as the trial allows so the latency overlaps other work
+__device__ __forceinline__ TaskRegs load_tasks(const LsState& S, int kmask) {
+    // task 1 kept from the previous rejected Move1 trial (set only inside a phase-1 Move1 loop)
+    if (S.c1_valid && S.nts == 2) kmask &= ~2;
+    TaskRegs r;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        tn[k] = k < S.nts && ((kmask >> k) & 1) ? S.misc[4 + k] : 0;
-        const bool a = S.lane < tn[k] && tn[k] <= 64;
-        tev[k] = a ? get_task(S, k).ev[S.lane] : 0;
-        tpl[k] = a ? S.pb.poss[tev[k]] : 0ull;
+        r.tn[k] = k < S.nts && ((kmask >> k) & 1) ? S.misc[4 + k] : 0;
+        const bool a = S.lane < r.tn[k] && r.tn[k] <= 64;
+        r.tev[k] = a ? get_task(S, k).ev[S.lane] : 0;
+        r.tpl[k] = a ? S.pb.poss[r.tev[k]] : 0ull;
     }
+    return r;
+}
+
+__device__ __forceinline__ bool match_tasks(LsState& S, int kmask, const TaskRegs& tr) {
+    if (S.c1_valid && S.nts == 2) kmask &= ~2;
+    if (!(kmask & ((1 << S.nts) - 1))) return false;            // nothing to match: no sync
+    LSP_T(t0);
+    const int* tn = tr.tn;
+    const int* tev = tr.tev;
+    const uint64_t* tpl = tr.tpl;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         if (k >= S.nts) break;
@@ -436,6 +449,10 @@ __device__ __forceinline__ bool match_tasks(LsState& S, int kmask) {
     wave_sync();
     LSP_ADD(S, kPfBuild, t0);
     return S.misc[3] != 0;
+}
+
+__device__ __forceinline__ bool match_tasks(LsState& S, int kmask) {
+    return match_tasks(S, kmask, load_tasks(S, kmask));
 }
 
 __device__ __forceinline__ bool build_and_match(LsState& S) {
@@ -673,10 +690,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         // task 0 = t plus ei, task 1 = t_orig minus ei (kept across trials).
                         // n = corr + misc[1] + misc[0] >= corr + misc[1]: a trial that cannot
                         // win is rejected before the target slot is matched.
+                        const TaskRegs tr0 = load_tasks(S, 1);
                         if (match_tasks(S, 2)) goto redo;
                         const int lb = corr_nb(S, ei) + S.misc[1];
                         if (lb >= c) { S.c1_valid = 1; continue; }
-                        if (match_tasks(S, 1)) goto redo;
+                        if (match_tasks(S, 1, tr0)) goto redo;
                         if (lb + S.misc[0] < c) { accept(S); evc = 0; better = true; break; }
                     } else {
                         if (match_tasks(S, 7)) goto redo;
@@ -697,13 +715,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         const int c = eah_cur(S, ei) + eah_cur(S, ej);
                         set_move(S, 2, ei, ej, 0);
                         build_nb(S);
+                        const TaskRegs tr = load_tasks(S, 7);
                         const int lb = corr_nb(S, ei) + corr_nb(S, ej);    // n >= lb whatever the rooms
                         if (lb >= c) continue;
                         if (S.nts == 2) {             // task 0 = slot(ej) plus ei, task 1 = slot(ei) plus ej
-                            if (match_tasks(S, 1)) goto redo;
+                            if (match_tasks(S, 1, tr)) goto redo;
                             if (lb + S.misc[0] >= c) { restore_task<0>(S); continue; }
-                            if (match_tasks(S, 2)) goto redo;
-                        } else if (match_tasks(S, 7)) goto redo;
+                            if (match_tasks(S, 2, tr)) goto redo;
+                        } else if (match_tasks(S, 7, tr)) goto redo;
                         const int n = lb + S.misc[task_of(S, slot_nb(S, ei))] + S.misc[task_of(S, slot_nb(S, ej))];
                         if (n < c) { accept(S); evc = 0; better = true; break; }
                         sync_rooms(S, false);
@@ -763,8 +782,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                     // eah_nb(ei) == 0 needs no correlated event in t (no rooms needed)
                     // and no room clash in t (task 0); the old slot (task 1) is
                     // matched only for an accepted move
+                    const TaskRegs tr = load_tasks(S, 1);
                     if (corr_nb(S, ei) != 0) continue;
-                    if (match_tasks(S, 1)) goto redo;
+                    if (match_tasks(S, 1, tr)) goto redo;
                     if (S.misc[0] == 0) {
                         int es_n, scs_n;
                         scv_terms(S, ei, true, es_n, scs_n);
@@ -786,12 +806,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         const int ej = S.evl[j];
                         set_move(S, 2, ei, ej, 0);
                         build_nb(S);
+                        const TaskRegs tr = load_tasks(S, 7);
                         if (corr_nb(S, ei) + corr_nb(S, ej) != 0) continue;   // eah_nb > 0 whatever the rooms
                         if (S.nts == 2) {
-                            if (match_tasks(S, 1)) goto redo;
+                            if (match_tasks(S, 1, tr)) goto redo;
                             if (S.misc[0] != 0) { restore_task<0>(S); continue; }
-                            if (match_tasks(S, 2)) goto redo;
-                        } else if (match_tasks(S, 7)) goto redo;
+                            if (match_tasks(S, 2, tr)) goto redo;
+                        } else if (match_tasks(S, 7, tr)) goto redo;
                         if (S.misc[task_of(S, slot_nb(S, ei))] + S.misc[task_of(S, slot_nb(S, ej))] == 0) {
                             int es_ni, scs_ni, es_nj, scs_nj, es_cj, scs_cj;
                             scv_terms(S, ei, true, es_ni, scs_ni);
