@@ -105,6 +105,7 @@ struct LsState {
     // for every target slot, so its matching is kept from one rejected trial
     // to the next (c1_valid) instead of being recomputed
     int c1_valid;
+    int listed;          // task event lists built for the current neighbour
 #ifdef TT_LS_PROF
     uint64_t prof[kPfN];
 #endif
@@ -359,7 +360,16 @@ __device__ __forceinline__ void build_nb(LsState& S) {
             S.NB[(size_t)k * EW + w] = x;
         }
     }
+    S.listed = 0;
     wave_sync();
+    LSP_ADD(S, kPfBuild, t0);
+}
+
+// Lists the events of each touched slot for the matcher (lane k lists slot k);
+// done only for trials that reach a matching.
+__device__ __forceinline__ void list_tasks(LsState& S) {
+    LSP_T(t0);
+    const int EW = S.EW;
     if (S.lane < S.nts) {
         const int k = S.lane;
         const LsTask T = get_task(S, k);
@@ -386,9 +396,13 @@ struct TaskRegs {
 
 // every task's events and possible rooms into registers at once (one L2 round
 // trip), issued as early as the trial allows so the latency overlaps other work
-__device__ __forceinline__ TaskRegs load_tasks(const LsState& S, int kmask) {
+__device__ __forceinline__ TaskRegs load_tasks(LsState& S, int kmask) {
     // task 1 kept from the previous rejected Move1 trial (set only inside a phase-1 Move1 loop)
     if (S.c1_valid && S.nts == 2) kmask &= ~2;
+    if (!S.listed) {
+        list_tasks(S);
+        S.listed = 1;
+    }
     TaskRegs r;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -452,6 +466,8 @@ __device__ __forceinline__ bool match_tasks(LsState& S, int kmask, const TaskReg
 }
 
 __device__ __forceinline__ bool match_tasks(LsState& S, int kmask) {
+    if (S.c1_valid && S.nts == 2) kmask &= ~2;
+    if (!(kmask & ((1 << S.nts) - 1))) return false;            // nothing to match: no listing, no loads
     return match_tasks(S, kmask, load_tasks(S, kmask));
 }
 
@@ -609,6 +625,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
     S.NT = L.NT;
     S.nmv = 0; S.nts = 0;
     S.c1_valid = 0;
+    S.listed = 0;
 #ifdef TT_LS_PROF
 #pragma unroll
     for (int i = 0; i < kPfN; ++i) S.prof[i] = 0;
@@ -690,11 +707,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         // task 0 = t plus ei, task 1 = t_orig minus ei (kept across trials).
                         // n = corr + misc[1] + misc[0] >= corr + misc[1]: a trial that cannot
                         // win is rejected before the target slot is matched.
-                        const TaskRegs tr0 = load_tasks(S, 1);
                         if (match_tasks(S, 2)) goto redo;
                         const int lb = corr_nb(S, ei) + S.misc[1];
                         if (lb >= c) { S.c1_valid = 1; continue; }
-                        if (match_tasks(S, 1, tr0)) goto redo;
+                        if (match_tasks(S, 1)) goto redo;
                         if (lb + S.misc[0] < c) { accept(S); evc = 0; better = true; break; }
                     } else {
                         if (match_tasks(S, 7)) goto redo;
@@ -715,9 +731,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         const int c = eah_cur(S, ei) + eah_cur(S, ej);
                         set_move(S, 2, ei, ej, 0);
                         build_nb(S);
-                        const TaskRegs tr = load_tasks(S, 7);
                         const int lb = corr_nb(S, ei) + corr_nb(S, ej);    // n >= lb whatever the rooms
                         if (lb >= c) continue;
+                        const TaskRegs tr = load_tasks(S, 7);
                         if (S.nts == 2) {             // task 0 = slot(ej) plus ei, task 1 = slot(ei) plus ej
                             if (match_tasks(S, 1, tr)) goto redo;
                             if (lb + S.misc[0] >= c) { restore_task<0>(S); continue; }
@@ -782,9 +798,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                     // eah_nb(ei) == 0 needs no correlated event in t (no rooms needed)
                     // and no room clash in t (task 0); the old slot (task 1) is
                     // matched only for an accepted move
-                    const TaskRegs tr = load_tasks(S, 1);
                     if (corr_nb(S, ei) != 0) continue;
-                    if (match_tasks(S, 1, tr)) goto redo;
+                    if (match_tasks(S, 1)) goto redo;
                     if (S.misc[0] == 0) {
                         int es_n, scs_n;
                         scv_terms(S, ei, true, es_n, scs_n);
@@ -806,8 +821,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         const int ej = S.evl[j];
                         set_move(S, 2, ei, ej, 0);
                         build_nb(S);
-                        const TaskRegs tr = load_tasks(S, 7);
                         if (corr_nb(S, ei) + corr_nb(S, ej) != 0) continue;   // eah_nb > 0 whatever the rooms
+                        const TaskRegs tr = load_tasks(S, 7);
                         if (S.nts == 2) {
                             if (match_tasks(S, 1, tr)) goto redo;
                             if (S.misc[0] != 0) { restore_task<0>(S); continue; }
