@@ -694,6 +694,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
             const int ei = S.evl[i];
             LSP_CNT(S, kPfVisits);
             if (ehcv_cur(S, ei) == 0) { evc++; continue; }
+            // eventAffectedHcv(ei) in the current state: unchanged until a trial is
+            // accepted, and every acceptance leaves this event's loops
+            const int eah_i = eah_cur(S, ei);
             const int t_start = pm_pick(st, kSlots);
             const int t_orig = S.sl[ei];
             for (int h = 0, t = t_start; h < kSlots; t = (t + 1) % kSlots, h++) {
@@ -702,7 +705,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                     step++;
                     set_move(S, 1, ei, t, 0);
                     build_nb(S);
-                    const int c = eah_cur(S, ei) + S.rp[t];
+                    const int c = eah_i + S.rp[t];
                     if (S.nts == 2) {
                         // task 0 = t plus ei, task 1 = t_orig minus ei (kept across trials).
                         // n = corr + misc[1] + misc[0] >= corr + misc[1]: a trial that cannot
@@ -728,7 +731,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                     if (pm_next(st) < p2) {
                         step++;
                         const int ej = S.evl[j];
-                        const int c = eah_cur(S, ei) + eah_cur(S, ej);
+                        const int c = eah_i + eah_cur(S, ej);
                         set_move(S, 2, ei, ej, 0);
                         build_nb(S);
                         const int lb = corr_nb(S, ei) + corr_nb(S, ej);    // n >= lb whatever the rooms
@@ -754,7 +757,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         const int ej = S.evl[j], ek = S.evl[k];
                         if (pm_next(st) < p3) {
                             step++;
-                            const int c = eah_cur(S, ei) + eah_cur(S, ej) + eah_cur(S, ek);
+                            const int c = eah_i + eah_cur(S, ej) + eah_cur(S, ek);
                             set_move(S, 3, ei, ej, ek);
                             if (build_and_match(S)) goto redo;
                             const int n = eah_nb(S, ei) + eah_nb(S, ej) + eah_nb(S, ek);
@@ -764,7 +767,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         if (step > max_steps) break;
                         if (pm_next(st) < p3) {
                             step++;
-                            const int c = eah_cur(S, ei) + eah_cur(S, ek) + eah_cur(S, ej);
+                            const int c = eah_i + eah_cur(S, ek) + eah_cur(S, ej);
                             set_move(S, 3, ei, ek, ej);
                             if (build_and_match(S)) goto redo;
                             const int n = eah_nb(S, ei) + eah_nb(S, ek) + eah_nb(S, ej);
