@@ -44,8 +44,10 @@ typedef struct tt_problem tt_problem;
 
 /* Replaces Problem::Problem(istream&) (Problem.cpp:3-96) and the MPI problem
  * broadcast (ga.cpp:417-426): takes the parsed .tim matrices, derives
- * studentNumber, eventCorrelations and possibleRooms exactly as
- * Problem.cpp:86-148, and uploads the device image to `device`.
+ * studentNumber (Problem.cpp:33-40), eventCorrelations (:42-58) and
+ * possibleRooms (:76-95) exactly as the reference, and uploads the device
+ * image to `device`. The derivation runs on the host in O(sum over students
+ * of deg^2) instead of the reference's O(E^2 S) (timed in tools/time_problem.py).
  *   room_size[R], student_events[S*E] (row-major, 0/1), room_features[R*F],
  *   event_features[E*F] (0/1). */
 int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, const int32_t* student_events,
@@ -87,7 +89,8 @@ int tt_eval(const tt_problem* p, const uint8_t* slot, const uint8_t* room, int P
 int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const uint8_t* room, int P, int32_t* hcv,
                     int32_t* scv, uint8_t* feasible, int32_t* penalty, int variant, void* stream);
 
-/* The variant tt_eval chooses for this instance (1..8), or -1 for a null handle. */
+/* The variant tt_eval chooses for this instance: 8 (E <= 448), 13 (the wide
+ * path, E <= 2490), else 2 (eval_block); -1 for a null handle. */
 int tt_eval_auto_variant(const tt_problem* p);
 
 /* Solution::assignRooms (Solution.cpp:772-891) on every non-empty timeslot in
@@ -138,15 +141,27 @@ size_t tt_ga_work_bytes(int N, int E);
 /* tt_ga_replace: the C evaluated children overwrite population positions
  * N-C..N-1 (ga.cpp:582, "pop[popSize-1]->copy(child)" for C = 1), then the
  * population is sorted by penalty ascending (ga.cpp:583; ties keep position
- * order, std::sort leaves them unspecified). In place; `work` has
- * tt_ga_work_bytes(N, E) bytes. */
+ * order, std::sort leaves them unspecified). Penalties compare as unsigned,
+ * so an invalid genome (penalty -1) sorts last; tt_ga_breed's selection5
+ * ranks it last the same way. In place; `work` has tt_ga_work_bytes(N, E)
+ * bytes. On return the first 8 bytes of `work` hold the sort key of the new
+ * pop[0]: its low 32 bits are the merged position it came from (N-C+c for
+ * child c), which the drivers use as the logEntry threadID. */
 int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* pop_room, int32_t* pop_hcv, int32_t* pop_scv,
                   uint8_t* pop_feasible, int32_t* pop_penalty, int N, const uint8_t* child_slot,
                   const uint8_t* child_room, const int32_t* child_hcv, const int32_t* child_scv,
                   const uint8_t* child_feasible, const int32_t* child_penalty, int C, void* work, void* stream);
 
-/* Device-side status word of the problem handle (0 = fine; bit 0 = a slot
- * exceeded 256 events in a matching). Synchronises the device. */
+/* Device-side status word of the problem handle (sticky, OR of):
+ *   bit 0 (1)  a slot exceeded 256 events in a matching; its rooms were written as 255;
+ *   bit 1 (2)  tt_local_search met an invalid genome (slot >= 45 or room >= R) and
+ *              left that individual untouched;
+ *   bit 2 (4)  tt_local_search's loop bound fired. Unreachable: a visit either
+ *              counts towards evCount < E or accepts a move, which costs a step,
+ *              so a phase makes at most (maxSteps + 2) * E visits
+ *              (Solution.cpp:498-505,616-618) and the bound is twice that per
+ *              phase; tests assert it never fires.
+ * Synchronises the device. */
 int tt_device_status(const tt_problem* p, int32_t* status);
 
 const char* tt_last_error(void);

@@ -50,16 +50,16 @@ struct Problem {
     int p(int e, int r) const { return possible[(size_t)e * R + r]; }
 };
 
-// Derived matrices, Problem.cpp:86-148.
+// Derived matrices, Problem.cpp:33-95.
 void derive(Problem& P) {
     const int E = P.E, R = P.R, F = P.F, S = P.S;
     P.student_number.assign(E, 0);
-    for (int i = 0; i < E; i++) {                       // Problem.cpp:87-93
+    for (int i = 0; i < E; i++) {                       // Problem.cpp:33-40
         int sum = 0;
         for (int j = 0; j < S; j++) sum += P.a(j, i);
         P.student_number[i] = sum;
     }
-    // Problem.cpp:96-111: corr[i][j] = 1 iff some student k has A[k][i]==1 and
+    // Problem.cpp:42-58: corr[i][j] = 1 iff some student k has A[k][i]==1 and
     // A[k][j]==1 (diagonal included). Restated student-major (same set, the
     // E*E*S triple loop is 108 s at E=2000,S=5000): for each student, mark
     // every ordered pair of the events it attends.
@@ -72,7 +72,7 @@ void derive(Problem& P) {
         for (size_t x = 0; x < ev.size(); x++)
             for (size_t y = 0; y < ev.size(); y++) P.corr[(size_t)ev[x] * E + ev[y]] = 1;
     }
-    P.possible.assign((size_t)E * R, 0);                // Problem.cpp:130-148
+    P.possible.assign((size_t)E * R, 0);                // Problem.cpp:76-95
     for (int i = 0; i < E; i++) {
         for (int j = 0; j < R; j++) {
             if (P.room_size[j] >= P.student_number[i]) {
@@ -742,7 +742,7 @@ void tto_ga_breed(const void* p, const uint8_t* pop_slot, const uint8_t* pop_roo
             int best = (int)(pm_next(&st) * N);
             for (int i = 1; i < 5; i++) {
                 int t = (int)(pm_next(&st) * N);
-                if (pen[t] < pen[best]) best = t;
+                if ((uint32_t)pen[t] < (uint32_t)pen[best]) best = t;   // invalid (-1) ranks last
             }
             par[q] = best;
         }
@@ -770,7 +770,8 @@ void tto_ga_breed(const void* p, const uint8_t* pop_slot, const uint8_t* pop_roo
 }
 
 // children overwrite positions N-C..N-1 (ga.cpp:582), then a stable sort by
-// penalty (ga.cpp:583).
+// penalty (ga.cpp:583). Penalties compare as unsigned: the -1 of an invalid
+// genome (tt_eval's sentinel, which the reference cannot produce) ranks last.
 void tto_ga_replace(const void* p, uint8_t* pop_slot, uint8_t* pop_room, int32_t* hcv, int32_t* scv, uint8_t* feas,
                     int32_t* pen, int N, const uint8_t* cs, const uint8_t* cr, const int32_t* ch, const int32_t* csc,
                     const uint8_t* cf, const int32_t* cp, int C) {
@@ -783,7 +784,7 @@ void tto_ga_replace(const void* p, uint8_t* pop_slot, uint8_t* pop_room, int32_t
     }
     std::vector<int> idx(N);
     for (int i = 0; i < N; i++) idx[i] = i;
-    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return pen[a] < pen[b]; });
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return (uint32_t)pen[a] < (uint32_t)pen[b]; });
     std::vector<uint8_t> s2((size_t)N * E), r2((size_t)N * E), f2(N);
     std::vector<int32_t> h2(N), sc2(N), p2(N);
     for (int i = 0; i < N; i++) {

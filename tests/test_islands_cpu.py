@@ -45,29 +45,33 @@ def test_json_line_matches_jsoncpp_format():
         '{"logEntry":{"best":12,"procID":0,"threadID":1,"time":0.10000000000000001}}'
 
 
-class FakeIsland:
-    """CPU stand-in with the Island migration interface (pack / unpack_into)."""
+def host_island(g, N=6, E=5):
+    """A real ttga.ga.Members population on CPU tensors (the same pack /
+    unpack_into payload code the device islands use), distinct per island g."""
+    from ttga.ga import Members, new_population
+    pop = new_population(N, E, torch.device("cpu"))
+    for k in range(N):
+        pop["slot"][k] = torch.tensor([(g * 61 + k * 11 + e) % 45 for e in range(E)], dtype=torch.uint8)
+        pop["room"][k] = torch.tensor([(g * 7 + k + e) % 10 for e in range(E)], dtype=torch.uint8)
+        pop["hcv"][k] = g * 100 + k
+        pop["scv"][k] = 1000 + g * 10 + k
+        pop["feasible"][k] = (g + k) % 2
+        pop["penalty"][k] = 1000000 * ((g + k) % 2 == 0) + 7 * k + g
+    return Members(pop)
 
-    def __init__(self, rank, N=6, E=5):
-        self.N, self.E = N, E
-        self.rows = torch.tensor([[(rank * 61 + k * 11 + e) % 256 for e in range(2 * E + 16)] for k in range(N)],
-                                 dtype=torch.uint8)
 
-    def pack(self, k):
-        return self.rows[k].clone()
-
-    def unpack_into(self, pos, buf):
-        self.rows[pos].copy_(buf)
+def snapshot(isl):
+    return [isl.pack(k).numpy().copy() for k in range(isl.N)]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, K, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    isl = FakeIsland(rank)
-    before = isl.rows.clone()
-    ring_migrate(isl, rank, world)
-    m = global_min(1000 + 7 * (world - rank), torch.device("cpu"), world)
-    q.put((rank, before.numpy(), isl.rows.numpy(), m))
+    isl = [host_island(rank * K + k) for k in range(K)]
+    before = [snapshot(i) for i in isl]
+    ring_migrate(isl, rank, world, backend="gloo")
+    m = global_min(1000 + 7 * (world - rank), torch.device("cpu"), world, backend="gloo")
+    q.put((rank, before, [snapshot(i) for i in isl], m))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -78,26 +82,44 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_ring_migration_gloo(world):
+def test_ring_migration_local_islands():
+    """K islands in one process: the ring is local copies (world 1)."""
+    K = 4
+    isl = [host_island(g) for g in range(K)]
+    before = [snapshot(i) for i in isl]
+    ring_migrate(isl, 0, 1)
+    N = isl[0].N
+    for g in range(K):
+        after = snapshot(isl[g])
+        assert np.array_equal(after[N - 1], before[(g - 1) % K][0])
+        assert np.array_equal(after[N - 2], before[(g + 1) % K][1])
+        assert all(np.array_equal(after[k], before[g][k]) for k in range(N - 2))
+    # unpack restores every field of the payload
+    m = isl[1].member(N - 1)
+    assert (m["hcv"], m["scv"], m["penalty"]) == (0, 1000, 1000000)
+
+
+@pytest.mark.parametrize("world,K", [(2, 1), (3, 1), (2, 3)])
+def test_ring_migration_gloo(world, K):
+    """world ranks x K islands each, real Members payloads over gloo."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, K, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = {}
+    before, after = {}, {}
     for _ in range(world):
-        r, before, after, m = q.get(timeout=120)
-        res[r] = (before, after, m)
+        r, b, a, m = q.get(timeout=120)
+        assert m == 1007                                        # MIN over ranks
+        for k in range(K):
+            before[r * K + k], after[r * K + k] = b[k], a[k]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    N = res[0][0].shape[0]
-    for r in range(world):
-        before, after, m = res[r]
-        left, right = (r - 1) % world, (r + 1) % world
-        assert np.array_equal(after[N - 1], res[left][0][0])    # best of the left neighbour
-        assert np.array_equal(after[N - 2], res[right][0][1])   # 2nd best of the right neighbour
-        assert np.array_equal(after[:N - 2], before[:N - 2])
-        assert m == 1007                                        # MIN over ranks
+    W = world * K
+    N = len(before[0])
+    for g in range(W):
+        assert np.array_equal(after[g][N - 1], before[(g - 1) % W][0])    # best of the left neighbour
+        assert np.array_equal(after[g][N - 2], before[(g + 1) % W][1])    # 2nd best of the right neighbour
+        assert all(np.array_equal(after[g][k], before[g][k]) for k in range(N - 2))

@@ -46,7 +46,7 @@ __global__ __launch_bounds__(64) void breed_kernel(int E, const uint8_t* __restr
             int b = pm_pick(s, N);
             for (int i = 1; i < 5; ++i) {
                 const int t = pm_pick(s, N);
-                if (pen[t] < pen[b]) b = t;
+                if ((uint32_t)pen[t] < (uint32_t)pen[b]) b = t;   // an invalid genome (-1) never wins
             }
             best[q] = b;
         }
@@ -90,8 +90,10 @@ __global__ __launch_bounds__(64) void breed_kernel(int E, const uint8_t* __restr
 }
 
 // ---------------------------------------------------------------- replace + sort
+// (penalty, position) as one u64; penalties compare as unsigned, so the -1 of an
+// invalid genome (tt_eval's sentinel; valid penalties are >= 0) sorts last
 __device__ __forceinline__ uint64_t sort_key(int32_t penalty, int pos) {
-    return ((uint64_t)((uint32_t)penalty ^ 0x80000000u) << 32) | (uint32_t)pos;
+    return ((uint64_t)(uint32_t)penalty << 32) | (uint32_t)pos;
 }
 
 // keys of the merged population: positions < N-C from pop, the rest from the children

@@ -686,6 +686,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
     LSP_ADD(S, kPfInit, t_kernel);
     int step = 0, evc = 0;
     bool better = false;
+    // Defensive bound on event visits, never reached: every visit either counts
+    // towards evc < E or accepts a trial (which costs a step and resets evc), so a
+    // phase makes at most (max_steps + 2) * E visits (Solution.cpp:498-505,616-618)
+    // and both phases together at most half of guard_max. Status bit 2 reports it;
+    // tests/test_gpu_parity.py asserts it never fires.
     const long guard_max = 4l * (long)E * ((long)max_steps + 2) + 1024;
     long guard = 0;
     if (!feasible_now(S)) {                                             // phase 1 (Solution.cpp:497-618)

@@ -1,5 +1,5 @@
 // Problem image: parse-free construction from .tim matrices, derived data
-// (Problem.cpp:86-148) and the device upload that replaces the reference's
+// (Problem.cpp:33-95) and the device upload that replaces the reference's
 // MPI_Pack/MPI_Bcast of the Problem (ga.cpp:264-309,417-426).
 #include <algorithm>
 #include <cstring>
@@ -65,7 +65,7 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     p->E = E; p->R = R; p->F = F; p->S = S; p->device = device;
     const int EW = (E + 31) / 32;
 
-    // studentNumber (Problem.cpp:87-93) and the two CSR views of student_events.
+    // studentNumber (Problem.cpp:33-40) and the two CSR views of student_events.
     std::vector<int32_t> stu_off(S + 1, 0), stu_ev, ev_off(E + 1, 0), ev_stu;
     p->student_number.assign(E, 0);
     for (int s = 0; s < S; s++) {
@@ -80,7 +80,7 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         for (int s = 0; s < S; s++)
             for (int k = stu_off[s]; k < stu_off[s + 1]; k++) ev_stu[cur[stu_ev[k]]++] = s;
     }
-    // eventCorrelations (Problem.cpp:96-111): i ~ j iff a student attends both
+    // eventCorrelations (Problem.cpp:42-58): i ~ j iff a student attends both
     // (diagonal set for events with students). Built student-major.
     p->corr_bits.assign((size_t)E * EW, 0u);
     for (int s = 0; s < S; s++)
@@ -160,7 +160,7 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         }
     }
     if (sch.empty()) sch.assign(8, 0);
-    // possibleRooms (Problem.cpp:130-148): size fits and every required feature present.
+    // possibleRooms (Problem.cpp:76-95): size fits and every required feature present.
     p->poss_bits.assign(E, 0ull);
     for (int i = 0; i < E; i++)
         for (int j = 0; j < R; j++) {

@@ -2,14 +2,17 @@
 // program over the C-ABI of include/ttga.h. One island per GPU of this node;
 // the MPI island model becomes RCCL over xGMI (one host thread and one
 // communicator rank per GPU, ncclCommInitAll), the OpenMP threads of a rank
-// become C children bred per batched generation.
+// become C children bred per batched generation. With --islands K != --gpus,
+// island g runs on GPU g % gpus and migrants move by device copies (the same
+// ring, no communicator): K islands can share one GPU.
 //
-//   ttga-ga -i instance.tim [-o out] [-s seed] [-p type] [-c children]
-//           [-p1 x -p2 y -p3 z] [--gpus K] [--pop N] [--generations G]
+//   ttga-ga -i instance.tim [-s seed] [-p type] [-c children]
+//           [-p1 x -p2 y -p3 z] [--gpus G] [--islands K] [--pop N] [--generations n]
 //
 // Reference correspondence:
 //  * CLI: `-key value` pairs and messages of Control::Control (Control.cpp:3-137);
-//    -n -t -m -l are parsed and echoed, then ignored, as in ga.cpp.
+//    -o -n -t -m -l are parsed and echoed, then ignored, as in ga.cpp (output
+//    always goes to stdout, ga.cpp:60).
 //  * -p -> maxSteps 200 / 1000 / 2000 (ga.cpp:389-397).
 //  * island k runs with seed abs(seed + k*(seed/10)) (ga.cpp:412); all islands
 //    start from island 0's initial population (ga.cpp:429-444,463-464).
@@ -17,7 +20,10 @@
 //    best -> right neighbour's pop[N-1], 2nd best -> left neighbour's pop[N-2]
 //    (ga.cpp:479-540); MIN all-reduce of the best value (ga.cpp:234-257);
 //    JSON lines of endTry / setCurrentCost / runEntry (ga.cpp:169-228,602-609)
-//    in jsoncpp's compact format (sorted keys, doubles as %.17g).
+//    in jsoncpp's compact format (sorted keys, doubles as %.17g); logEntry
+//    threadID = the child slot whose replacement made the new best (ga.cpp:584);
+//    logEntry/solution times from beginTry (ga.cpp:476), the last totalTime
+//    from process start (ga.cpp:381).
 //  * same stream layout as ttga/ga.py (Island): member i of the initial
 //    population draws from Random(|s|+1+i), child slot c from Random(|s|+1+N+c).
 #include <rccl/rccl.h>
@@ -71,19 +77,20 @@ struct Control {
     double time_limit = 90, ls_limit = 99999, p1 = 1.0, p2 = 1.0, p3 = 0.0;
     long seed = 0;
     std::string input, output;
-    int gpus = 1, pop = 10, generations = -1;
+    int gpus = 1, islands = 0, pop = 10, generations = -1;
 };
 
 // Control::Control (Control.cpp:3-137) plus the --gpus/--pop/--generations extensions.
 Control parse_control(int argc, char** argv) {
     std::vector<std::string> args(argv + 1, argv + argc);
     Control c;
-    for (const char* k : {"--gpus", "--pop", "--generations", "--children"}) {
+    for (const char* k : {"--gpus", "--islands", "--pop", "--generations", "--children"}) {
         auto it = std::find(args.begin(), args.end(), k);
         if (it != args.end()) {
             if (it + 1 == args.end()) die(std::string("missing value for ") + k);
             const int v = std::atoi((it + 1)->c_str());
             if (!std::strcmp(k, "--gpus")) c.gpus = v;
+            else if (!std::strcmp(k, "--islands")) c.islands = v;
             else if (!std::strcmp(k, "--pop")) c.pop = v;
             else if (!std::strcmp(k, "--generations")) c.generations = v;
             else c.threads = v;
@@ -285,7 +292,8 @@ struct Island {
     int64_t *rng_init = nullptr, *rng_child = nullptr;
     uint8_t* flags = nullptr;
     void* work = nullptr;
-    uint8_t *send_buf = nullptr, *recv_buf = nullptr;   // one migrant: slot[E] room[E] hcv scv penalty feasible
+    // migrants (ga.cpp:318-335): slot[E] room[E] hcv scv penalty feasible
+    uint8_t *send_best = nullptr, *send_second = nullptr, *recv_buf = nullptr;
     size_t migrant_bytes = 0;
     int best_scv = INT_MAX, best_eval = INT_MAX;      // setCurrentCost state (ga.cpp:163-167)
 
@@ -307,8 +315,9 @@ struct Island {
         check_hip(hipMalloc(&flags, (size_t)C), "hipMalloc");
         check_hip(hipMalloc(&work, std::max<size_t>(tt_ga_work_bytes(N, E), 16)), "hipMalloc");
         migrant_bytes = 2 * (size_t)E + 13;
-        check_hip(hipMalloc(&send_buf, migrant_bytes), "hipMalloc");
-        check_hip(hipMalloc(&recv_buf, migrant_bytes), "hipMalloc");
+        check_hip(hipMalloc(&send_best, migrant_bytes), "hipMalloc");
+        check_hip(hipMalloc(&send_second, migrant_bytes), "hipMalloc");
+        check_hip(hipMalloc(&recv_buf, 2 * migrant_bytes), "hipMalloc");
     }
 
     void evaluate(Pop& p) {
@@ -350,8 +359,19 @@ struct Island {
         return m;
     }
 
+    // the reference thread whose replacement put pop[0] in place (ga.cpp:580-585):
+    // child c of the last tt_ga_replace (the sort key it leaves in `work`), else 0
+    int best_thread(bool after_step) {
+        if (!after_step) return 0;
+        uint64_t key = 0;
+        check_hip(hipMemcpyAsync(&key, work, 8, hipMemcpyDeviceToHost, st), "hipMemcpy");
+        check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+        const long src = (long)(key & 0xFFFFFFFFull), k = N - C;
+        return src >= k && src < N ? (int)(src - k) : 0;
+    }
+
     // setCurrentCost (ga.cpp:203-228) on pop[0]
-    void log_cost(Output& out, std::chrono::steady_clock::time_point t0) {
+    void log_cost(Output& out, std::chrono::steady_clock::time_point t0, int thread) {
         const Member m = member(0);
         long entry = -1;
         if (m.feasible) {
@@ -364,14 +384,14 @@ struct Island {
             Json e;
             e.obj["best"] = Json::I(entry);
             e.obj["procID"] = Json::I(id);
-            e.obj["threadID"] = Json::I(0);
+            e.obj["threadID"] = Json::I(thread);
             e.obj["time"] = Json::D(std::max(0.0, seconds_since(t0)));
             out.line(wrap("logEntry", e));
         }
     }
 
     // serializeSolutions(k, 1, ...) (ga.cpp:318-342) into send_buf
-    void pack(int k) {
+    void pack(int k, uint8_t* send_buf) {
         auto cp = [&](void* dst, const void* src, size_t n) {
             check_hip(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
         };
@@ -399,7 +419,8 @@ struct Island {
     void release() {
         pop.release();
         child.release();
-        for (void* p : {(void*)rng_init, (void*)rng_child, (void*)flags, work, (void*)send_buf, (void*)recv_buf})
+        for (void* p : {(void*)rng_init, (void*)rng_child, (void*)flags, work, (void*)send_best, (void*)send_second,
+                        (void*)recv_buf})
             if (p) (void)hipFree(p);
         if (st) (void)hipStreamDestroy(st);
         if (tp) tt_problem_destroy(tp);
@@ -426,34 +447,32 @@ private:
 }  // namespace
 
 int main(int argc, char** argv) {
-    const auto t0 = std::chrono::steady_clock::now();
+    const auto t_start = std::chrono::steady_clock::now();
     Control ctl = parse_control(argc, argv);
-    std::ofstream file;
-    if (!ctl.output.empty()) {
-        file.open(ctl.output);
-        if (!file) die("cannot open " + ctl.output);
-    }
-    Output out(ctl.output.empty() ? std::cout : file);
+    Output out(std::cout);                       // ga.cpp:60: -o is parsed, output goes to cout
     const Instance inst = read_tim(ctl.input);
 
     int ndev = 0;
     check_hip(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
-    const int K = ctl.gpus;
-    if (K < 1 || K > ndev) die("--gpus " + std::to_string(K) + " but " + std::to_string(ndev) + " GPU(s) visible");
-    const int N = std::max(2, ctl.pop);
+    const int G = ctl.gpus;
+    if (G < 1 || G > ndev) die("--gpus " + std::to_string(G) + " but " + std::to_string(ndev) + " GPU(s) visible");
+    const int K = ctl.islands > 0 ? ctl.islands : G;
+    if (ctl.pop < 3) die("--pop must be at least 3 (ring migration writes pop[N-1] and pop[N-2])");
+    const int N = ctl.pop;
     const int C = std::max(1, std::min(ctl.threads, N));
     const int gens = ctl.generations >= 0 ? ctl.generations : (2001 + C - 1) / C;   // generations 0..2000 (ga.cpp:510)
+    const bool rccl = K == G && K > 1;           // one island per GPU: RCCL ring; otherwise device copies
 
     std::vector<Island> isl(K);
     for (int k = 0; k < K; k++) {
         Island& I = isl[k];
-        I.id = k; I.device = k; I.N = N; I.C = C;
+        I.id = k; I.device = k % G; I.N = N; I.C = C;
         I.max_steps = max_steps_for(ctl.problem_type);
         I.seed = island_seed(ctl.seed, k);
         I.p1 = ctl.p1; I.p2 = ctl.p2; I.p3 = ctl.p3;
     }
     std::vector<ncclComm_t> comms(K, nullptr);
-    if (K > 1) {
+    if (rccl) {
         std::vector<int> devs(K);
         for (int k = 0; k < K; k++) devs[k] = k;
         check_nccl(ncclCommInitAll(comms.data(), K, devs.data()), "ncclCommInitAll");
@@ -461,14 +480,17 @@ int main(int argc, char** argv) {
     Barrier barrier(K);
     std::vector<long> best_value(K, 0);
     std::vector<int> best_feasible(K, 0);
+    std::chrono::steady_clock::time_point t_begin;
 
+    auto sync = [](Island& I) { check_hip(hipStreamSynchronize(I.st), "hipStreamSynchronize"); };
     auto run = [&](int k) {
         Island& I = isl[k];
         I.setup(inst);
         if (k == 0) I.initialize();
-        if (K > 1) {   // every island starts from island 0's population (ga.cpp:442-464)
-            check_hip(hipStreamSynchronize(I.st), "hipStreamSynchronize");
-            barrier.wait();
+        sync(I);
+        barrier.wait();
+        // every island starts from island 0's population (ga.cpp:442-464)
+        if (rccl) {
             check_nccl(ncclGroupStart(), "ncclGroupStart");
             check_nccl(ncclBroadcast(I.pop.slot, I.pop.slot, (size_t)N * I.E, ncclUint8, 0, comms[k], I.st), "bcast");
             check_nccl(ncclBroadcast(I.pop.room, I.pop.room, (size_t)N * I.E, ncclUint8, 0, comms[k], I.st), "bcast");
@@ -477,33 +499,54 @@ int main(int argc, char** argv) {
             check_nccl(ncclBroadcast(I.pop.penalty, I.pop.penalty, N, ncclInt32, 0, comms[k], I.st), "bcast");
             check_nccl(ncclBroadcast(I.pop.feasible, I.pop.feasible, N, ncclUint8, 0, comms[k], I.st), "bcast");
             check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+        } else if (k > 0) {
+            const Pop& z = isl[0].pop;
+            auto cp = [&](void* dst, const void* src, size_t n) {
+                check_hip(hipMemcpyPeerAsync(dst, I.device, src, isl[0].device, n, I.st), "hipMemcpyPeerAsync");
+            };
+            cp(I.pop.slot, z.slot, (size_t)N * I.E);
+            cp(I.pop.room, z.room, (size_t)N * I.E);
+            cp(I.pop.hcv, z.hcv, 4 * (size_t)N);
+            cp(I.pop.scv, z.scv, 4 * (size_t)N);
+            cp(I.pop.penalty, z.penalty, 4 * (size_t)N);
+            cp(I.pop.feasible, z.feasible, (size_t)N);
         }
-        I.log_cost(out, t0);
+        sync(I);
+        barrier.wait();
+        if (k == 0) t_begin = std::chrono::steady_clock::now();      // beginTry (ga.cpp:476)
+        barrier.wait();
+        I.log_cost(out, t_begin, 0);
         const int right = (k + 1) % K, left = (k + K - 1) % K;
         for (int g = 0; g < gens; g++) {
             if ((g + 1) % 100 == 50) {   // ga.cpp:514-540, one migrant each way
-                check_hip(hipStreamSynchronize(I.st), "hipStreamSynchronize");
+                I.pack(0, I.send_best);                   // best, then 2nd best (N >= 3: untouched by dir 0)
+                I.pack(1, I.send_second);
+                sync(I);
                 barrier.wait();
-                for (int dir = 0; dir < 2; dir++) {
-                    const int src_rank = std::min(dir, N - 1);      // best, then 2nd best
-                    const int pos = N - 1 - dir;                    // pop[N-1], then pop[N-2]
-                    I.pack(src_rank);
-                    if (K == 1) {
-                        I.unpack(pos, I.send_buf);
-                        continue;
-                    }
-                    const int to = dir == 0 ? right : left, from = dir == 0 ? left : right;
+                uint8_t* from_left = I.recv_buf;          // dir 0: left's best -> pop[N-1]
+                uint8_t* from_right = I.recv_buf + I.migrant_bytes;   // dir 1: right's 2nd best -> pop[N-2]
+                if (rccl) {
                     check_nccl(ncclGroupStart(), "ncclGroupStart");
-                    check_nccl(ncclSend(I.send_buf, I.migrant_bytes, ncclUint8, to, comms[k], I.st), "ncclSend");
-                    check_nccl(ncclRecv(I.recv_buf, I.migrant_bytes, ncclUint8, from, comms[k], I.st), "ncclRecv");
+                    check_nccl(ncclSend(I.send_best, I.migrant_bytes, ncclUint8, right, comms[k], I.st), "ncclSend");
+                    check_nccl(ncclRecv(from_left, I.migrant_bytes, ncclUint8, left, comms[k], I.st), "ncclRecv");
                     check_nccl(ncclGroupEnd(), "ncclGroupEnd");
-                    I.unpack(pos, I.recv_buf);
+                    check_nccl(ncclGroupStart(), "ncclGroupStart");
+                    check_nccl(ncclSend(I.send_second, I.migrant_bytes, ncclUint8, left, comms[k], I.st), "ncclSend");
+                    check_nccl(ncclRecv(from_right, I.migrant_bytes, ncclUint8, right, comms[k], I.st), "ncclRecv");
+                    check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+                } else {
+                    check_hip(hipMemcpyPeerAsync(from_left, I.device, isl[left].send_best, isl[left].device,
+                                                 I.migrant_bytes, I.st), "hipMemcpyPeerAsync");
+                    check_hip(hipMemcpyPeerAsync(from_right, I.device, isl[right].send_second, isl[right].device,
+                                                 I.migrant_bytes, I.st), "hipMemcpyPeerAsync");
                 }
-                check_hip(hipStreamSynchronize(I.st), "hipStreamSynchronize");
-                barrier.wait();
+                I.unpack(N - 1, from_left);
+                I.unpack(N - 2, from_right);
+                sync(I);
+                barrier.wait();      // the neighbours' send buffers are free again
             }
             I.step();
-            I.log_cost(out, t0);
+            I.log_cost(out, t_begin, I.best_thread(true));
         }
         const Member b = I.member(0);
         best_feasible[k] = b.feasible;
@@ -513,9 +556,9 @@ int main(int argc, char** argv) {
     for (int k = 0; k < K; k++) th.emplace_back(run, k);
     for (auto& t : th) t.join();
 
-    // setGlobalCost (ga.cpp:234-257): MIN over islands through RCCL, printed by island 0
-    long gmin = best_value[0];
-    if (K > 1) {
+    // setGlobalCost (ga.cpp:234-257): MIN over islands (RCCL all-reduce across GPUs), printed once
+    long gmin = *std::min_element(best_value.begin(), best_value.end());
+    if (rccl) {
         std::vector<std::thread> red;
         std::vector<int32_t*> dv(K, nullptr);
         for (int k = 0; k < K; k++)
@@ -550,7 +593,7 @@ int main(int argc, char** argv) {
         s.obj["feasible"] = Json::B(b.feasible);
         s.obj["procID"] = Json::I(k);
         s.obj["threadID"] = Json::I(0);
-        s.obj["totalTime"] = Json::D(seconds_since(t0));
+        s.obj["totalTime"] = Json::D(seconds_since(t_begin));
         if (b.feasible) {
             s.obj["totalBest"] = Json::I(b.scv);
             std::vector<uint8_t> sl(I.E), rm(I.E);
@@ -567,7 +610,7 @@ int main(int argc, char** argv) {
         Json r;
         r.obj["procsNum"] = Json::I(K);
         r.obj["threadsNum"] = Json::I(C);
-        r.obj["totalTime"] = Json::D(seconds_since(t0));
+        r.obj["totalTime"] = Json::D(seconds_since(t_start));
         out.line(wrap("runEntry", r));
     }
     for (int k = 0; k < K; k++) {

@@ -62,7 +62,81 @@ def stream_seeds(seed: int, first: int, n: int) -> np.ndarray:
     return (np.arange(first, first + n, dtype=np.int64) + np.int64(abs(int(seed)) + 1)).astype(np.int64)
 
 
-class Island:
+def pack_member(pop: dict, k: int):
+    """serializeSolutions(k, 1, ...) (ga.cpp:318-335): one migrant as a flat
+    uint8 tensor on the population's device: slot[E], room[E], then int32
+    hcv, scv, feasible, penalty."""
+    import torch
+    meta = torch.stack([pop["hcv"][k], pop["scv"][k], pop["feasible"][k].to(torch.int32), pop["penalty"][k]])
+    return torch.cat([pop["slot"][k], pop["room"][k], meta.view(torch.uint8)])
+
+
+def unpack_member(pop: dict, pos: int, buf) -> None:
+    """deserializeSolution(offset, 1, ...) into position `pos` (ga.cpp:344-368).
+    `buf` may live on another device (a host-staged payload)."""
+    import torch
+    E = pop["slot"].shape[1]
+    buf = buf.to(pop["slot"].device)
+    pop["slot"][pos].copy_(buf[:E])
+    pop["room"][pos].copy_(buf[E:2 * E])
+    meta = buf[2 * E:2 * E + 16].clone().view(torch.int32)
+    pop["hcv"][pos] = meta[0]
+    pop["scv"][pos] = meta[1]
+    pop["feasible"][pos] = meta[2].to(torch.uint8)
+    pop["penalty"][pos] = meta[3]
+
+
+def new_population(n: int, E: int, device):
+    import torch
+    return {"slot": torch.zeros((n, E), dtype=torch.uint8, device=device),
+            "room": torch.zeros((n, E), dtype=torch.uint8, device=device),
+            "hcv": torch.zeros(n, dtype=torch.int32, device=device),
+            "scv": torch.zeros(n, dtype=torch.int32, device=device),
+            "feasible": torch.zeros(n, dtype=torch.uint8, device=device),
+            "penalty": torch.zeros(n, dtype=torch.int32, device=device)}
+
+
+class Members:
+    """A population [N] of (slot, room, hcv, scv, feasible, penalty) tensors
+    and the migration interface of ga.cpp (pack / unpack_into). Island adds
+    the device GA on top; the class itself works on any torch device, which
+    is what the CPU (gloo) tests of the ring use."""
+
+    min_pop = 3     # ring migration writes pop[N-1] and pop[N-2] and reads pop[0], pop[1]
+
+    def __init__(self, pop: dict):
+        self.pop = pop
+        self.N = int(pop["slot"].shape[0])
+
+    def pack(self, k: int):
+        return pack_member(self.pop, k)
+
+    def unpack_into(self, pos: int, buf) -> None:
+        unpack_member(self.pop, pos, buf)
+
+    def copy_from(self, other: "Members") -> None:
+        for k, t in self.pop.items():
+            t.copy_(other.pop[k].to(t.device))
+
+    def member(self, k: int) -> dict:
+        """deserialised Solution fields of member k (ga.cpp:318-335 payload)."""
+        p = self.pop
+        return {"slot": p["slot"][k].cpu().numpy(), "room": p["room"][k].cpu().numpy(),
+                "feasible": bool(p["feasible"][k].item()), "scv": int(p["scv"][k].item()),
+                "hcv": int(p["hcv"][k].item()), "penalty": int(p["penalty"][k].item())}
+
+    def member_meta(self, k: int):
+        p = self.pop
+        return (bool(p["feasible"][k].item()), int(p["scv"][k].item()), int(p["hcv"][k].item()),
+                int(p["penalty"][k].item()))
+
+    def best_value(self) -> tuple[bool, int]:
+        """(feasible, scv) if feasible else (False, hcv*1e6 + scv) (ga.cpp:191,218,247)."""
+        b = self.member_meta(0)
+        return (True, b[1]) if b[0] else (False, b[2] * 1000000 + b[1])
+
+
+class Island(Members):
     """One island: population [N] + C child slots, all device-resident."""
 
     def __init__(self, dp, pop_size: int = 10, children: int = 1, max_steps: int = 200, seed: int = 1,
@@ -71,22 +145,13 @@ class Island:
         import torch
         if not (1 <= children <= pop_size):
             raise ValueError("need 1 <= children <= pop_size")
-        self.dp, self.N, self.C = dp, int(pop_size), int(children)
+        dev = torch.device("cuda", dp.device if device is None else device)
+        super().__init__(new_population(int(pop_size), dp.E, dev))
+        self.dp, self.C = dp, int(children)
         self.max_steps, self.seed = int(max_steps), int(seed)
         self.p_cross, self.p_mut, self.skip = float(p_cross), float(p_mut), bool(skip_init_draws)
         self.p1, self.p2, self.p3 = float(p1), float(p2), float(p3)   # LS move probabilities (Solution.h:61)
-        dev = torch.device("cuda", dp.device if device is None else device)
-        E = dp.E
-
-        def pop(n):
-            return {"slot": torch.zeros((n, E), dtype=torch.uint8, device=dev),
-                    "room": torch.zeros((n, E), dtype=torch.uint8, device=dev),
-                    "hcv": torch.zeros(n, dtype=torch.int32, device=dev),
-                    "scv": torch.zeros(n, dtype=torch.int32, device=dev),
-                    "feasible": torch.zeros(n, dtype=torch.uint8, device=dev),
-                    "penalty": torch.zeros(n, dtype=torch.int32, device=dev)}
-
-        self.pop, self.child = pop(self.N), pop(self.C)
+        self.child = new_population(self.C, dp.E, dev)
         self.flags = torch.zeros(self.C, dtype=torch.uint8, device=dev)
         self.rng_init = torch.from_numpy(stream_seeds(seed, 0, self.N)).to(dev)
         self.rng_child = torch.from_numpy(stream_seeds(seed, self.N, self.C)).to(dev)
@@ -114,44 +179,13 @@ class Island:
         self.dp.ga_replace(self.pop, c, self.work)
         self.generation += 1
 
-    # -- host views ------------------------------------------------------------------
-    def member(self, k: int) -> dict:
-        """deserialised Solution fields of member k (ga.cpp:318-335 payload)."""
-        p = self.pop
-        return {"slot": p["slot"][k].cpu().numpy(), "room": p["room"][k].cpu().numpy(),
-                "feasible": bool(p["feasible"][k].item()), "scv": int(p["scv"][k].item()),
-                "hcv": int(p["hcv"][k].item()), "penalty": int(p["penalty"][k].item())}
-
-    def best_value(self) -> tuple[bool, int]:
-        """(feasible, scv) if feasible else (False, hcv*1e6 + scv) (ga.cpp:191,218,247)."""
-        b = self.member_meta(0)
-        return (True, b[1]) if b[0] else (False, b[2] * 1000000 + b[1])
-
-    def member_meta(self, k: int):
-        p = self.pop
-        return (bool(p["feasible"][k].item()), int(p["scv"][k].item()), int(p["hcv"][k].item()),
-                int(p["penalty"][k].item()))
-
-    # -- migration payloads (device tensors) ---------------------------------------------
-    def pack(self, k: int):
-        """One migrant as a flat uint8 device tensor: slot[E], room[E], meta int32[4]."""
-        import torch
-        p = self.pop
-        meta = torch.stack([p["hcv"][k], p["scv"][k], p["feasible"][k].to(torch.int32), p["penalty"][k]])
-        return torch.cat([p["slot"][k], p["room"][k], meta.view(torch.uint8)])
-
-    def unpack_into(self, pos: int, buf):
-        """deserializeSolution(offset) into population position `pos` (ga.cpp:344-368)."""
-        import torch
-        E = self.dp.E
-        p = self.pop
-        p["slot"][pos].copy_(buf[:E])
-        p["room"][pos].copy_(buf[E:2 * E])
-        meta = buf[2 * E:2 * E + 16].clone().view(torch.int32)
-        p["hcv"][pos] = meta[0]
-        p["scv"][pos] = meta[1]
-        p["feasible"][pos] = meta[2].to(torch.uint8)
-        p["penalty"][pos] = meta[3]
+    def best_thread(self) -> int:
+        """The reference thread (ga.cpp:498, one per child slot) whose
+        replacement put the current pop[0] in place: child c of the last
+        tt_ga_replace (its sort key, include/ttga.h), else thread 0."""
+        src = int(self.work[:8].view(__import__("torch").int64)[0].item()) & 0xFFFFFFFF
+        k = self.N - self.C
+        return src - k if self.generation > 0 and k <= src < self.N else 0
 
 
 class CostLog:

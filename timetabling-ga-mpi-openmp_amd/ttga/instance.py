@@ -48,7 +48,7 @@ class Instance:
         self.room_features = np.ascontiguousarray(self.room_features, dtype=np.int32).reshape(self.R, self.F)
         self.event_features = np.ascontiguousarray(self.event_features, dtype=np.int32).reshape(self.E, self.F)
 
-    # -- derived data, Problem.cpp:86-148 (numpy restatement, used by tests and the CLI)
+    # -- derived data, Problem.cpp:33-95 (numpy restatement, used by tests and the CLI)
     def student_number(self) -> np.ndarray:
         return self.student_events.sum(axis=0).astype(np.int32)
 

@@ -1,23 +1,34 @@
 """ga.cpp's driver on MI355X: one island per GPU, torch.distributed (RCCL over
-xGMI) for the island model.
+xGMI) for the island model; optionally K islands multiplexed on each GPU.
 
-    python -m ttga.islands -i instance.tim -s 42 -p 1 [-c C] [--pop N]
+    python -m ttga.islands -i instance.tim -s 42 -p 1 [-c C] [--pop N] [--islands K]
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
         -m ttga.islands -i instance.tim -s 42 -p 1
 
 Reference correspondence:
-* CLI: `-key value` pairs as Control.cpp:3-137; honoured: -i -o -p -s -c
+* CLI: `-key value` pairs as Control.cpp:3-137; honoured: -i -p -s -c
   (as ga.cpp) plus -p1 -p2 -p3 (LS move probabilities, a documented superset);
-  -n -t -m -l are parsed and echoed like Control.cpp, then ignored like ga.cpp.
-  `-c` (threads) sets the children bred per generation. `--pop` sets the
-  population size (ga.cpp:64 has 10).
-* seeds: rank i uses abs(seed + i*(seed/10)) (ga.cpp:410-415).
-* every island starts from rank 0's initial population (ga.cpp:429-444,463-464).
+  -o -n -t -m -l are parsed and echoed like Control.cpp, then ignored like
+  ga.cpp (every JSON line goes to stdout, ga.cpp:60). `-c` (threads) sets the
+  children bred per generation. Extensions: `--pop N` (ga.cpp:64 has 10,
+  N >= 3), `--islands K` (islands per process, default 1), `--generations G`,
+  `--backend nccl|gloo` (gloo stages migrants through host memory; with it
+  several ranks may share one GPU).
+* islands: island g = rank*K + k of W = world*K; seed abs(seed + g*(seed/10))
+  (ga.cpp:410-415), the base seed chosen by rank 0 (time(NULL) when -s is
+  missing, ga.cpp:401) and broadcast; procID = g.
+* every island starts from island 0's initial population (ga.cpp:429-444,463-464).
 * 2001 children per island (generations 0..2000 of ga.cpp:510), migration
-  before generations g with (g+1) % 100 == 50 (ga.cpp:514): best -> right
-  neighbour's pop[N-1], 2nd best -> left neighbour's pop[N-2] (ga.cpp:479-540).
-* setGlobalCost MIN all-reduce (ga.cpp:234-257), endTry per rank (ga.cpp:169-197),
-  final runEntry (ga.cpp:602-609). JSON lines in the reference's format.
+  before generations g with (g+1) % 100 == 50 (ga.cpp:514): best -> island
+  (g+1) % W's pop[N-1], 2nd best -> island (g-1) % W's pop[N-2]
+  (ga.cpp:479-540); within a process the ring is local copies, across ranks
+  one batched send/recv pair per direction.
+* setCurrentCost per island with threadID = the child slot (thread) whose
+  replacement produced the new best (ga.cpp:203-228,584); setGlobalCost MIN
+  all-reduce (ga.cpp:234-257), endTry per island (ga.cpp:169-197), final
+  runEntry (ga.cpp:602-609). logEntry/solution times run from beginTry
+  (ga.cpp:476, after the initial population is shared), the final totalTime
+  from process start (ga.cpp:381). JSON lines in the reference's format.
 """
 from __future__ import annotations
 
@@ -34,7 +45,7 @@ def parse_control(argv, out=sys.stdout, err=sys.stderr) -> dict:
     """Control::Control (Control.cpp:3-137): `-key value` pairs."""
     args = list(argv)
     extra = {}
-    for k in ("--pop", "--children", "--generations"):
+    for k in ("--pop", "--children", "--generations", "--islands"):
         if k in args:
             i = args.index(k)
             extra[k[2:]] = int(args[i + 1])
@@ -94,43 +105,78 @@ def rank_seed(seed: int, rank: int) -> int:
     return abs(seed + rank * q)
 
 
-def ring_migrate(island, rank: int, world: int):
-    """ga.cpp:514-540 with one migrant each way: best -> (rank+1) replaces its
-    pop[N-1]; 2nd best -> (rank-1) replaces its pop[N-2]."""
+def _wire(t, backend: str):
+    """Payload as the process group can move it: gloo moves host tensors."""
+    return t.cpu() if backend == "gloo" else t
+
+
+def _exchange(send, dst: int, src: int, backend: str):
     import torch
     import torch.distributed as dist
-    N = island.N
-    snd, rcv = (rank + 1) % world, (rank - 1 + world) % world
-    for k, dst, src, pos in ((0, snd, rcv, N - 1), (1, rcv, snd, N - 2)):
-        if pos < 0:
-            continue
-        buf = island.pack(min(k, N - 1)).contiguous()
-        if world == 1:
-            island.unpack_into(pos, buf.clone())
-            continue
-        got = torch.empty_like(buf)
-        ops = [dist.P2POp(dist.isend, buf, dst), dist.P2POp(dist.irecv, got, src)]
-        for r in dist.batch_isend_irecv(ops):
-            r.wait()
-        island.unpack_into(pos, got)
+    buf = _wire(send.contiguous(), backend)
+    got = torch.empty_like(buf)
+    for r in dist.batch_isend_irecv([dist.P2POp(dist.isend, buf, dst), dist.P2POp(dist.irecv, got, src)]):
+        r.wait()
+    return got
 
 
-def global_min(value: int, device, world: int) -> int:
+def ring_migrate(islands, rank: int, world: int, backend: str = "nccl"):
+    """ga.cpp:514-540 with one migrant each way over the ring of all W =
+    world * K islands (island g = rank * K + k): g's best replaces pop[N-1] of
+    island (g+1) % W, g's 2nd best replaces pop[N-2] of island (g-1) % W. All
+    payloads are packed before any is written (MPI_Sendrecv semantics; with
+    N >= 3 the rows read and written are disjoint, as in the reference)."""
+    if not isinstance(islands, (list, tuple)):
+        islands = [islands]
+    K, N = len(islands), islands[0].N
+    if N < 3:
+        raise ValueError("ring migration needs a population of at least 3")
+    best = [isl.pack(0) for isl in islands]
+    second = [isl.pack(1) for isl in islands]
+    if world == 1:
+        from_left, from_right = best[-1], second[0]
+    else:
+        right, left = (rank + 1) % world, (rank - 1 + world) % world
+        from_left = _exchange(best[-1], right, left, backend)
+        from_right = _exchange(second[0], left, right, backend)
+    for k, isl in enumerate(islands):
+        isl.unpack_into(N - 1, best[k - 1] if k > 0 else from_left)
+        isl.unpack_into(N - 2, second[k + 1] if k < K - 1 else from_right)
+
+
+def global_min(value: int, device, world: int, backend: str = "nccl") -> int:
     import torch
     import torch.distributed as dist
     if world == 1:
         return int(value)
-    t = torch.tensor([int(value)], dtype=torch.int64, device=device)
+    t = torch.tensor([int(value)], dtype=torch.int64, device=device if backend != "gloo" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return int(t.item())
 
 
-def broadcast_population(island, world: int):
+def share_seed(seed, world: int) -> int:
+    """Rank 0's base seed on every rank (ga.cpp:401,410-415)."""
     import torch.distributed as dist
     if world == 1:
-        return
-    for t in island.pop.values():
-        dist.broadcast(t, src=0)
+        return int(seed)
+    lst = [int(seed)]
+    dist.broadcast_object_list(lst, src=0)
+    return int(lst[0])
+
+
+def broadcast_population(islands, world: int, backend: str = "nccl"):
+    """Island 0 of rank 0 to every island (ga.cpp:436-444,461-464)."""
+    import torch.distributed as dist
+    if world > 1:
+        for t in islands[0].pop.values():
+            if backend == "gloo" and t.is_cuda:
+                h = t.cpu()
+                dist.broadcast(h, src=0)
+                t.copy_(h)
+            else:
+                dist.broadcast(t, src=0)
+    for isl in islands[1:]:
+        isl.copy_from(islands[0])
 
 
 def main(argv=None):
@@ -139,58 +185,83 @@ def main(argv=None):
 
     from . import instance as tim
     from .ga import CostLog, Island, json_line, max_steps_for
+
     from .native import DeviceProblem
 
+    t_start = time.perf_counter()
     argv = sys.argv[1:] if argv is None else argv
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = "nccl"
+    if "--backend" in argv:
+        i = argv.index("--backend")
+        backend = argv[i + 1]
+        argv = argv[:i] + argv[i + 2:]
+    device = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    t0 = time.perf_counter()
-    ctl = parse_control(argv, out=sys.stdout if rank == 0 else open(os.devnull, "w"))
-    out = open(ctl["output"], "w") if ctl.get("output") else sys.stdout
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
+    ctl = parse_control(argv, out=sys.stdout if rank == 0 else open(os.devnull, "w"),
+                        err=sys.stderr if rank == 0 else open(os.devnull, "w"))
+    out = sys.stdout                 # ga.cpp:60: -o is parsed, output always goes to cout
+    seed = share_seed(ctl["seed"], world)
     inst = tim.read_tim(ctl["input"])
-    dp = DeviceProblem(inst, device=local)
+    dp = DeviceProblem(inst, device=device)
     C = ctl.get("children", ctl["threads"])
     N = ctl.get("pop", 10)
+    if N < 3:
+        sys.stderr.write("Error: --pop must be at least 3 (ring migration writes pop[N-1] and pop[N-2])\n")
+        raise SystemExit(1)
     C = max(1, min(C, N))
-    island = Island(dp, pop_size=N, children=C, max_steps=max_steps_for(ctl["problem_type"]),
-                    seed=rank_seed(ctl["seed"], rank), p1=ctl["p1"], p2=ctl["p2"], p3=ctl["p3"])
+    K = max(1, ctl.get("islands", 1))
+    W = world * K
+    islands = [Island(dp, pop_size=N, children=C, max_steps=max_steps_for(ctl["problem_type"]),
+                      seed=rank_seed(seed, rank * K + k), p1=ctl["p1"], p2=ctl["p2"], p3=ctl["p3"])
+               for k in range(K)]
     if rank == 0:
-        island.initialize()
-    broadcast_population(island, world)
-    log = CostLog(rank, out, t0)
-    log.update(island)
+        islands[0].initialize()
+    broadcast_population(islands, world, backend)
+    torch.cuda.synchronize()
+    t_begin = time.perf_counter()    # beginTry (ga.cpp:476)
+    logs = [CostLog(rank * K + k, out, t_begin) for k in range(K)]
+    for log, isl in zip(logs, islands):
+        log.update(isl, 0)           # ga.cpp:503
     gens = ctl.get("generations", math.ceil(TOTAL_CHILDREN / C))
     for g in range(gens):
         if (g + 1) % 100 == 50:
             if world > 1:
                 dist.barrier()
-            ring_migrate(island, rank, world)
-        island.step()
-        log.update(island)
+            ring_migrate(islands, rank, world, backend)
+        for log, isl in zip(logs, islands):
+            isl.step()
+            log.update(isl, isl.best_thread())
     torch.cuda.synchronize()
-    feasible, value = island.best_value()
-    gmin = global_min(value, torch.device("cuda", local), world)
+    vals = [isl.best_value() for isl in islands]
+    gmin = global_min(min(v for _, v in vals), torch.device("cuda", device), world, backend)
     if rank == 0:
-        out.write(json_line({"runEntry": {"feasible": feasible, "totalBest": gmin}}) + "\n")
-    best = island.member(0)
-    sol = {"feasible": best["feasible"], "procID": rank, "threadID": 0,
-           "totalTime": time.perf_counter() - t0}
-    if best["feasible"]:
-        sol["totalBest"] = best["scv"]
-        sol["timeslots"] = [int(x) for x in best["slot"]]
-        sol["rooms"] = [int(x) for x in best["room"]]
-    else:
-        sol["totalBest"] = best["hcv"] * 1000000 + best["scv"]
-    out.write(json_line({"solution": sol}) + "\n")
+        # setGlobalCost: "feasible" is rank 0's own pop[0] (ga.cpp:236-256)
+        out.write(json_line({"runEntry": {"feasible": vals[0][0], "totalBest": gmin}}) + "\n")
+    for k, isl in enumerate(islands):
+        best = isl.member(0)
+        sol = {"feasible": best["feasible"], "procID": rank * K + k, "threadID": 0,
+               "totalTime": time.perf_counter() - t_begin}
+        if best["feasible"]:
+            sol["totalBest"] = best["scv"]
+            sol["timeslots"] = [int(x) for x in best["slot"]]
+            sol["rooms"] = [int(x) for x in best["room"]]
+        else:
+            sol["totalBest"] = best["hcv"] * 1000000 + best["scv"]
+        out.write(json_line({"solution": sol}) + "\n")
+    out.flush()
     if world > 1:
         dist.barrier()
     if rank == 0:
-        out.write(json_line({"runEntry": {"procsNum": world, "threadsNum": C,
-                                          "totalTime": time.perf_counter() - t0}}) + "\n")
+        out.write(json_line({"runEntry": {"procsNum": W, "threadsNum": C,
+                                          "totalTime": time.perf_counter() - t_start}}) + "\n")
     out.flush()
     if world > 1:
         dist.destroy_process_group()

@@ -128,6 +128,8 @@ class DeviceProblem:
     # -- population operations (torch tensors on this device) -------------------
     @staticmethod
     def _stream(t):
+        # note: every library call makes the handle's device current (hipSetDevice)
+        # and leaves it so; tensors of another device are rejected by _pop/_rng
         import torch
         return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
@@ -138,6 +140,8 @@ class DeviceProblem:
                 continue
             if not (t.is_cuda and t.dtype == torch.uint8 and t.is_contiguous() and t.dim() == 2 and t.shape[1] == self.E):
                 raise ValueError("population tensors must be contiguous uint8 CUDA tensors of shape [P, E]")
+            if t.device.index != self.device:
+                raise ValueError(f"tensor on cuda:{t.device.index}, problem handle on cuda:{self.device}")
         return slot.shape[0]
 
     def eval(self, slot, room, variant: int = 0, out=None):
@@ -200,7 +204,8 @@ class DeviceProblem:
 
     def ga_work(self, N):
         import torch
-        return torch.empty(int(self.lib.tt_ga_work_bytes(N, self.E)), dtype=torch.uint8, device="cuda")
+        return torch.empty(int(self.lib.tt_ga_work_bytes(N, self.E)), dtype=torch.uint8,
+                           device=torch.device("cuda", self.device))
 
     def ga_replace(self, pop, child, work):
         """pop/child: dicts of device tensors slot, room, hcv, scv, feasible, penalty."""
