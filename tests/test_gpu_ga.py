@@ -190,3 +190,33 @@ def test_ga_trajectories_match_reference_statistically(sm):
     assert stats.fisher_exact(table)[1] > 0.01
     p = stats.mannwhitneyu(dfinal, rtrace[:, -1], alternative="two-sided").pvalue
     assert p > 0.01, (dfinal, rtrace[:, -1], p)
+
+
+@pytest.mark.parametrize("c", range(4))
+def test_breed_selection5_vs_reference(sm, c):
+    """tt_ga_breed's tournaments against the reference's own selection5
+    (tests/golden/ga_ref.json, ga.cpp:129-145 compiled from the reference):
+    with crossover always on, child k's slots follow parent a = winner 2k and
+    parent b = winner 2k+1 of the golden sequence."""
+    from test_json_parity import GOLD, selection_case_expectations
+    from ttga.rng import ParkMiller
+    inst, dp, o = sm
+    case = GOLD["selection5"][c]
+    N = case["N"]
+    rng = np.random.default_rng(c)
+    pop_slot = rng.integers(0, 45, (N, inst.E), dtype=np.uint8)
+    pop_room = o.assign_rooms(pop_slot)
+    seeds = selection_case_expectations(case)
+    C = seeds.size
+    gs, gr = dev(np.zeros((C, inst.E), np.uint8)), dev(np.zeros((C, inst.E), np.uint8))
+    gf, grng = dev(np.zeros(C, np.uint8)), dev(seeds)
+    dp.ga_breed(dev(pop_slot), dev(pop_room), dev(np.array(case["penalty"], np.int32)), grng, gs, gr, gf, 1.0, 0.0,
+                False)
+    got = host(gs)
+    w = np.array(case["winners"])
+    for k in range(C):
+        pm = ParkMiller(int(seeds[k]))
+        for _ in range(11):
+            pm.next()
+        take_a = np.array([pm.next() < 0.5 for _ in range(inst.E)])
+        assert np.array_equal(got[k], np.where(take_a, pop_slot[w[2 * k]], pop_slot[w[2 * k + 1]])), k

@@ -242,6 +242,96 @@ Json wrap(const char* key, Json inner) {
     return j;
 }
 
+// The four JSON line kinds of ga.cpp, shared by the driver and --replay-log.
+// setCurrentCost state (ga.cpp:57-58, reset by beginTry :163-167) and decision (:203-228):
+// feasible pop[0] logs when its scv differs from the last logged best,
+// infeasible when hcv*1e6+scv is lower.
+struct CostState {
+    long best_scv = INT_MAX, best_eval = INT_MAX;
+    bool offer(bool feasible, int scv, int hcv, long& entry) {
+        if (feasible) {
+            if (scv == best_scv) return false;
+            best_scv = best_eval = entry = scv;
+            return true;
+        }
+        const long ev = (long)hcv * 1000000 + scv;
+        if (ev >= best_eval) return false;
+        best_eval = entry = ev;
+        return true;
+    }
+};
+
+Json log_line(long best, int proc, int thread, double t) {
+    Json e;
+    e.obj["best"] = Json::I(best);
+    e.obj["procID"] = Json::I(proc);
+    e.obj["threadID"] = Json::I(thread);
+    e.obj["time"] = Json::D(std::max(0.0, t));
+    return wrap("logEntry", e);
+}
+
+// setGlobalCost (ga.cpp:234-257), printed by rank 0
+Json run_best_line(bool feasible, long total_best) {
+    Json r;
+    r.obj["feasible"] = Json::B(feasible);
+    r.obj["totalBest"] = Json::I(total_best);
+    return wrap("runEntry", r);
+}
+
+// endTry (ga.cpp:169-197); threadID is the global tid, 0 outside the parallel region
+Json solution_line(bool feasible, int scv, int hcv, const std::vector<uint8_t>& sl, const std::vector<uint8_t>& rm,
+                   int proc, double t) {
+    Json s;
+    s.obj["feasible"] = Json::B(feasible);
+    s.obj["procID"] = Json::I(proc);
+    s.obj["threadID"] = Json::I(0);
+    s.obj["totalTime"] = Json::D(t);
+    if (feasible) {
+        s.obj["totalBest"] = Json::I(scv);
+        s.obj["timeslots"] = Json::A(std::vector<long>(sl.begin(), sl.end()));
+        s.obj["rooms"] = Json::A(std::vector<long>(rm.begin(), rm.end()));
+    } else {
+        s.obj["totalBest"] = Json::I((long)hcv * 1000000 + scv);
+    }
+    return wrap("solution", s);
+}
+
+// main's closing runEntry (ga.cpp:603-609)
+Json run_final_line(int procs, int threads, double t) {
+    Json r;
+    r.obj["procsNum"] = Json::I(procs);
+    r.obj["threadsNum"] = Json::I(threads);
+    r.obj["totalTime"] = Json::D(t);
+    return wrap("runEntry", r);
+}
+
+// ttga-ga --replay-log FILE: the lines one island prints when its pop[0] takes
+// the given values in turn (no GPU involved; tests/test_json_parity.py checks
+// them against the reference's own ga.cpp + jsoncpp). FILE: "proc threads n E",
+// n lines "feasible scv hcv tid", then the last member's E slots and E rooms.
+// Times print as 0 (the last runEntry: 0.5).
+int replay_log(const char* path) {
+    std::ifstream in(path);
+    if (!in) die(std::string("cannot open ") + path);
+    int proc = 0, threads = 1, n = 0, E = 0;
+    if (!(in >> proc >> threads >> n >> E) || n < 1 || E < 0) die("bad replay header");
+    CostState cs;
+    int f = 0, scv = 0, hcv = 0, tid = 0;
+    for (int i = 0; i < n; i++) {
+        if (!(in >> f >> scv >> hcv >> tid)) die("truncated replay file");
+        long entry = 0;
+        if (cs.offer(f != 0, scv, hcv, entry)) std::cout << log_line(entry, proc, tid, 0.0).str() << "\n";
+    }
+    std::vector<uint8_t> sl(E), rm(E);
+    for (int e = 0; e < E; e++) { int v; in >> v; sl[e] = (uint8_t)v; }
+    for (int e = 0; e < E; e++) { int v; in >> v; rm[e] = (uint8_t)v; }
+    if (!in) die("truncated replay file");
+    if (proc == 0) std::cout << run_best_line(f != 0, f ? scv : (long)hcv * 1000000 + scv).str() << "\n";
+    std::cout << solution_line(f != 0, scv, hcv, sl, rm, proc, 0.0).str() << "\n";
+    std::cout << run_final_line(1, threads, 0.5).str() << std::endl;
+    return 0;
+}
+
 // ---------------------------------------------------------------- islands
 struct Pop {
     int n = 0, E = 0;
@@ -295,7 +385,7 @@ struct Island {
     // migrants (ga.cpp:318-335): slot[E] room[E] hcv scv penalty feasible
     uint8_t *send_best = nullptr, *send_second = nullptr, *recv_buf = nullptr;
     size_t migrant_bytes = 0;
-    int best_scv = INT_MAX, best_eval = INT_MAX;      // setCurrentCost state (ga.cpp:163-167)
+    CostState cost;                                   // setCurrentCost state (ga.cpp:163-167)
 
     void setup(const Instance& inst) {
         check_hip(hipSetDevice(device), "hipSetDevice");
@@ -373,21 +463,8 @@ struct Island {
     // setCurrentCost (ga.cpp:203-228) on pop[0]
     void log_cost(Output& out, std::chrono::steady_clock::time_point t0, int thread) {
         const Member m = member(0);
-        long entry = -1;
-        if (m.feasible) {
-            if (m.scv != best_scv) { best_scv = best_eval = m.scv; entry = m.scv; }
-        } else {
-            const long ev = (long)m.hcv * 1000000 + m.scv;
-            if (ev < best_eval) { best_eval = (int)ev; entry = ev; }
-        }
-        if (entry >= 0) {
-            Json e;
-            e.obj["best"] = Json::I(entry);
-            e.obj["procID"] = Json::I(id);
-            e.obj["threadID"] = Json::I(thread);
-            e.obj["time"] = Json::D(std::max(0.0, seconds_since(t0)));
-            out.line(wrap("logEntry", e));
-        }
+        long entry = 0;
+        if (cost.offer(m.feasible, m.scv, m.hcv, entry)) out.line(log_line(entry, id, thread, seconds_since(t0)));
     }
 
     // serializeSolutions(k, 1, ...) (ga.cpp:318-342) into send_buf
@@ -448,6 +525,7 @@ private:
 
 int main(int argc, char** argv) {
     const auto t_start = std::chrono::steady_clock::now();
+    if (argc == 3 && !std::strcmp(argv[1], "--replay-log")) return replay_log(argv[2]);
     Control ctl = parse_control(argc, argv);
     Output out(std::cout);                       // ga.cpp:60: -o is parsed, output goes to cout
     const Instance inst = read_tim(ctl.input);
@@ -578,41 +656,18 @@ int main(int argc, char** argv) {
         gmin = v;
         for (int k = 0; k < K; k++) { (void)hipSetDevice(k); (void)hipFree(dv[k]); }
     }
-    {
-        Json r;
-        r.obj["feasible"] = Json::B(best_feasible[0] != 0);
-        r.obj["totalBest"] = Json::I(gmin);
-        out.line(wrap("runEntry", r));
-    }
+    out.line(run_best_line(best_feasible[0] != 0, gmin));
     // endTry (ga.cpp:169-197) per island
     for (int k = 0; k < K; k++) {
         Island& I = isl[k];
         check_hip(hipSetDevice(I.device), "hipSetDevice");
         const Member b = I.member(0);
-        Json s;
-        s.obj["feasible"] = Json::B(b.feasible);
-        s.obj["procID"] = Json::I(k);
-        s.obj["threadID"] = Json::I(0);
-        s.obj["totalTime"] = Json::D(seconds_since(t_begin));
-        if (b.feasible) {
-            s.obj["totalBest"] = Json::I(b.scv);
-            std::vector<uint8_t> sl(I.E), rm(I.E);
-            check_hip(hipMemcpy(sl.data(), I.pop.slot, I.E, hipMemcpyDeviceToHost), "hipMemcpy");
-            check_hip(hipMemcpy(rm.data(), I.pop.room, I.E, hipMemcpyDeviceToHost), "hipMemcpy");
-            s.obj["timeslots"] = Json::A(std::vector<long>(sl.begin(), sl.end()));
-            s.obj["rooms"] = Json::A(std::vector<long>(rm.begin(), rm.end()));
-        } else {
-            s.obj["totalBest"] = Json::I((long)b.hcv * 1000000 + b.scv);
-        }
-        out.line(wrap("solution", s));
+        std::vector<uint8_t> sl(I.E), rm(I.E);
+        check_hip(hipMemcpy(sl.data(), I.pop.slot, I.E, hipMemcpyDeviceToHost), "hipMemcpy");
+        check_hip(hipMemcpy(rm.data(), I.pop.room, I.E, hipMemcpyDeviceToHost), "hipMemcpy");
+        out.line(solution_line(b.feasible, b.scv, b.hcv, sl, rm, k, seconds_since(t_begin)));
     }
-    {
-        Json r;
-        r.obj["procsNum"] = Json::I(K);
-        r.obj["threadsNum"] = Json::I(C);
-        r.obj["totalTime"] = Json::D(seconds_since(t_start));
-        out.line(wrap("runEntry", r));
-    }
+    out.line(run_final_line(K, C, seconds_since(t_start)));
     for (int k = 0; k < K; k++) {
         (void)hipSetDevice(isl[k].device);
         isl[k].release();

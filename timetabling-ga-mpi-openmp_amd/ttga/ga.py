@@ -189,17 +189,18 @@ class Island(Members):
 
 
 class CostLog:
-    """setCurrentCost (ga.cpp:203-228): a logEntry line whenever pop[0] changes the best."""
+    """setCurrentCost (ga.cpp:203-228): a logEntry line whenever pop[0] changes
+    the island's best (feasible: scv differs; infeasible: hcv*1e6+scv lower)."""
 
     def __init__(self, proc_id: int, out, t0: float):
         self.proc_id, self.out, self.t0 = proc_id, out, t0
-        self.best_scv = 2 ** 31 - 1
+        self.best_scv = 2 ** 31 - 1          # beginTry (ga.cpp:163-167)
         self.best_eval = 2 ** 31 - 1
 
-    def update(self, island: Island, thread_id: int = 0):
-        feas, scv, hcv, _ = island.member_meta(0)
+    def offer(self, feasible: bool, scv: int, hcv: int, thread_id: int = 0, t: float | None = None):
+        """pop[0] now has these fields; returns the logged line or None."""
         entry = None
-        if feas:
+        if feasible:
             if scv != self.best_scv:
                 self.best_scv = scv
                 self.best_eval = scv
@@ -209,7 +210,38 @@ class CostLog:
             if ev < self.best_eval:
                 self.best_eval = ev
                 entry = ev
-        if entry is not None and self.out is not None:
+        if entry is None:
+            return None
+        if t is None:
             t = max(0.0, time.perf_counter() - self.t0)
-            self.out.write(json_line({"logEntry": {"best": entry, "procID": self.proc_id, "threadID": thread_id,
-                                                   "time": t}}) + "\n")
+        line = json_line({"logEntry": {"best": entry, "procID": self.proc_id, "threadID": thread_id, "time": t}})
+        if self.out is not None:
+            self.out.write(line + "\n")
+        return line
+
+    def update(self, island, thread_id: int = 0):
+        feas, scv, hcv, _ = island.member_meta(0)
+        return self.offer(feas, scv, hcv, thread_id)
+
+
+def run_best_line(feasible: bool, total_best: int) -> str:
+    """setGlobalCost's line (ga.cpp:234-257), printed by rank 0."""
+    return json_line({"runEntry": {"feasible": bool(feasible), "totalBest": int(total_best)}})
+
+
+def solution_line(best: dict, proc_id: int, total_time: float) -> str:
+    """endTry (ga.cpp:169-197) for pop[0] = `best` (Members.member fields);
+    threadID is the global tid, 0 outside the parallel region."""
+    sol = {"feasible": bool(best["feasible"]), "procID": int(proc_id), "threadID": 0, "totalTime": float(total_time)}
+    if best["feasible"]:
+        sol["totalBest"] = int(best["scv"])
+        sol["timeslots"] = [int(x) for x in best["slot"]]
+        sol["rooms"] = [int(x) for x in best["room"]]
+    else:
+        sol["totalBest"] = int(best["hcv"]) * 1000000 + int(best["scv"])
+    return json_line({"solution": sol})
+
+
+def run_final_line(procs: int, threads: int, total_time: float) -> str:
+    """main's closing runEntry (ga.cpp:603-609)."""
+    return json_line({"runEntry": {"procsNum": int(procs), "threadsNum": int(threads), "totalTime": float(total_time)}})

@@ -184,7 +184,7 @@ def main(argv=None):
     import torch.distributed as dist
 
     from . import instance as tim
-    from .ga import CostLog, Island, json_line, max_steps_for
+    from .ga import CostLog, Island, max_steps_for, run_best_line, run_final_line, solution_line
 
     from .native import DeviceProblem
 
@@ -244,24 +244,14 @@ def main(argv=None):
     gmin = global_min(min(v for _, v in vals), torch.device("cuda", device), world, backend)
     if rank == 0:
         # setGlobalCost: "feasible" is rank 0's own pop[0] (ga.cpp:236-256)
-        out.write(json_line({"runEntry": {"feasible": vals[0][0], "totalBest": gmin}}) + "\n")
+        out.write(run_best_line(vals[0][0], gmin) + "\n")
     for k, isl in enumerate(islands):
-        best = isl.member(0)
-        sol = {"feasible": best["feasible"], "procID": rank * K + k, "threadID": 0,
-               "totalTime": time.perf_counter() - t_begin}
-        if best["feasible"]:
-            sol["totalBest"] = best["scv"]
-            sol["timeslots"] = [int(x) for x in best["slot"]]
-            sol["rooms"] = [int(x) for x in best["room"]]
-        else:
-            sol["totalBest"] = best["hcv"] * 1000000 + best["scv"]
-        out.write(json_line({"solution": sol}) + "\n")
+        out.write(solution_line(isl.member(0), rank * K + k, time.perf_counter() - t_begin) + "\n")
     out.flush()
     if world > 1:
         dist.barrier()
     if rank == 0:
-        out.write(json_line({"runEntry": {"procsNum": W, "threadsNum": C,
-                                          "totalTime": time.perf_counter() - t_start}}) + "\n")
+        out.write(run_final_line(W, C, time.perf_counter() - t_start) + "\n")
     out.flush()
     if world > 1:
         dist.destroy_process_group()
