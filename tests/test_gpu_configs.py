@@ -243,11 +243,9 @@ def test_islands_drivers_multiplexed_lg(tmp_path, orc):
     assert runs[-1]["procsNum"] == 8 and runs[-1]["threadsNum"] == 2
     sols = [v[-1]["solution"] for v in a[0].values()]
     assert runs[0]["totalBest"] == min(s["totalBest"] for s in sols)
-    o = orc.problem(inst)
-    for s in sols:
-        if s["feasible"]:
-            h, sc, f, p = o.eval(np.array(s["timeslots"], np.uint8)[None], np.array(s["rooms"], np.uint8)[None])
-            assert f[0] == 1 and sc[0] == s["totalBest"]
+    from test_gpu_ga import assert_validated
+    assert_validated(inst, tim, py.stdout)
+    assert_validated(inst, tim, cc.stdout)
     threads = {e["logEntry"]["threadID"] for v in a[0].values() for e in v if "logEntry" in e}
     assert threads <= {0, 1}
 
@@ -277,3 +275,5 @@ def test_islands_two_ranks_gloo_one_gpu(tmp_path):
     assert two.returncode == 0, two.stderr[-3000:]
     a, b = _lines(one.stdout), _lines(two.stdout)
     assert sorted(a[0]) == [0, 1, 2, 3] and a == b
+    from test_gpu_ga import assert_validated
+    assert_validated(inst, tim, two.stdout)
