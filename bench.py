@@ -3,13 +3,17 @@ penalty, Solution.cpp:63-170) of a device-resident population of 65,536
 individuals on the 400-event medium01-size instance, per GPU (weak scaling:
 one independent population shard per rank, no data-path collective).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config med|lg|syn|sm]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 A step is one tt_eval over the rank's whole population. Rank 0 prints one JSON
 line (BASELINE.json metric) with the dominant kernel's roofline and, at N=1, a
 CPU baseline: the reference's own computeFeasibility/Hcv/Scv (oracle/_ref,
-OpenMP over individuals) timed on a bounded sample of the same population.
+OpenMP over individuals on every core this job may use) timed on a bounded
+sample of the same population. At N=1 the roofline's `traffic` and the LDS /
+VALU / SALU busy fractions are measured live: before this process touches the
+GPU, three short child runs of the same workload under `rocprofv3 --pmc`
+(tools/pmc_live.py) read FETCH_SIZE, WRITE_SIZE and the SQ counters.
 """
 from __future__ import annotations
 
@@ -49,13 +53,40 @@ def parse():
                     help="individuals in the CPU-baseline sample (0: sized to about --cpu-seconds of CPU work)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 counter passes")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+def host_cores():
+    """Cores this job may use (affinity, cgroup CPU quota), the machine's
+    total and the CPU model (/proc/cpuinfo)."""
+    total = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = total
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            avail = min(avail, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return avail, total, model
 
 
 def cpu_baseline(inst, slot_np, room_np, gpu_out):
     """The reference's evaluation (oracle/_ref) or, without it, the oracle port."""
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    from oracle_lib import REF_PATH, oracle, ref
+    threads, total, model = host_cores()
+    from oracle_lib import oracle, ref
     n = slot_np.shape[0]
     hcv = np.zeros(n, np.int32); scv = np.zeros(n, np.int32)
     feas = np.zeros(n, np.uint8); pen = np.zeros(n, np.int32)
@@ -77,29 +108,32 @@ def cpu_baseline(inst, slot_np, room_np, gpu_out):
     agree = all(np.array_equal(a, b[:n]) for a, b in zip((hcv, scv, feas, pen), gpu_out))
     return {"value": n / secs, "unit": "evals/s", "cores": cores, "kind": kind,
             "sample": f"{n} individuals of the same population, computeFeasibility+computeHcv+computeScv+penalty, "
-                      f"OpenMP dynamic over individuals, {secs:.2f} s", "matches_gpu": bool(agree)}
+                      f"OpenMP dynamic over individuals, {secs:.2f} s", "matches_gpu": bool(agree),
+            "cpu_model": model, "host_cores_total": total,
+            "cores_note": "every core this job may use (affinity and cgroup quota); the GPU box grants one GPU's share"}
 
 
-def pmc_traffic(workload_key):
-    f = REPO / "profiles" / "pmc_traffic.json"
-    if not f.exists():
-        return None
-    try:
-        d = json.loads(f.read_text())
-        return d.get(workload_key)
-    except Exception:
-        return None
+DOMINANT = {8: "eval_tile5_kernel", 13: "eval_", 2: "eval_block_kernel"}   # kernel name substrings
 
 
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    pmc = None
+    if world == 1 and not args.no_pmc and not args.pmc_child:
+        # live counters of the same workload, before this process initialises the GPU
+        sys.path.insert(0, str(REPO / "tools"))
+        import pmc_live
+        child = [str(REPO / "bench.py"), "--pmc-child", "--config", args.config, "--pop", str(args.pop),
+                 "--steps", "20", "--warmup", "2", "--variant", str(args.variant)]
+        pmc = pmc_live.derive(pmc_live.collect(child, DOMINANT.get(args.variant or
+                                                                   (8 if args.config != "syn" else 13), "eval_")))
     import torch
     import torch.distributed as dist
 
     import ttga
     from ttga import native
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -146,14 +180,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
 
+    if args.pmc_child:
+        return
     if rank == 0:
         total = P * world * args.steps
         value = total / wall_max
         bytes_per_eval = 2 * E + 13                     # u8 slot+room in; i32 hcv,scv,penalty + u8 feasible out
         achieved = bytes_per_eval * P / (kernel_ms * 1e-3) / 1e9
         variant = args.variant or dp.eval_variant()
-        wkey = f"{args.config}_P{P}_v{variant}"
-        tr = pmc_traffic(wkey)
         line = {
             "metric": METRIC, "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": wall_max / args.steps * 1e3, "higher_is_better": True,
@@ -164,9 +198,15 @@ def main():
                        "kernel": KERNELS[variant],
                        "parallelism": f"dp{world} (independent population shards)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": tr,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None if pmc is None else pmc["traffic_bytes"],
+                         "traffic_unit": "bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, live rocprofv3 pass)",
+                         "algorithmic_bytes": bytes_per_eval * P,
                          "kernel_ms": kernel_ms, "bytes_per_eval": bytes_per_eval},
         }
+        if pmc is not None:
+            line["roofline"]["pipes"] = {k: pmc[k] for k in ("lds_busy", "lds_conflict", "valu_busy", "salu_busy",
+                                                            "wait_any", "cycles") if k in pmc}
         if world == 1 and not args.no_cpu:
             n = args.cpu_sample
             if n <= 0:      # calibrate on a small slice, then size the sample to ~cpu_seconds
@@ -174,7 +214,7 @@ def main():
                 c = cpu_baseline(inst, slot[:n0].cpu().numpy(), room[:n0].cpu().numpy(),
                                  [o[:n0].cpu().numpy() for o in out])
                 n = int(max(n0, min(P, c["value"] * args.cpu_seconds)))
-            n = min(n, P)
+            n = min(max(n, 2048), P)              # at least 2,048 individuals
             s_np, r_np = slot[:n].cpu().numpy(), room[:n].cpu().numpy()
             gpu_out = [o[:n].cpu().numpy() for o in out]
             line["cpu_baseline"] = cpu_baseline(inst, s_np, r_np, gpu_out)

@@ -1,0 +1,58 @@
+"""Start-up cost of the Problem image (Problem.cpp:3-96).
+
+Times, per configuration: the .tim parse (ttga.instance.read_tim), the whole
+tt_problem_create (host derivation of studentNumber / eventCorrelations /
+possibleRooms in O(sum of deg^2) plus the single device upload), and, where
+oracle/_ref is present, the reference's own Problem(istream&) (its
+eventCorrelations triple loop is O(E^2 S): 108 s at syn in the survey).
+
+    python tools/time_problem.py [out.json]
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import pathlib
+import sys
+import tempfile
+import time
+
+REPO = pathlib.Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(REPO / "timetabling-ga-mpi-openmp_amd"), str(REPO / "tests")]
+
+import ttga  # noqa: E402
+from ttga import native  # noqa: E402
+
+
+def main():
+    out = {}
+    native.DeviceProblem(ttga.config_instance("sm"))           # HIP initialisation, not timed
+    from oracle_lib import ref
+    R = ref()
+    for name in ("med", "lg", "comp01", "syn"):
+        inst = ttga.config_instance(name)
+        with tempfile.TemporaryDirectory() as d:
+            path = pathlib.Path(d) / f"{name}.tim"
+            ttga.write_tim(inst, path)
+            t = time.perf_counter()
+            inst2 = ttga.read_tim(path)
+            parse = time.perf_counter() - t
+            t = time.perf_counter()
+            dp = native.DeviceProblem(inst2)
+            create = time.perf_counter() - t
+            row = {"E": inst.E, "R": inst.R, "F": inst.F, "S": inst.S, "parse_s": parse,
+                   "tt_problem_create_s": create}
+            if R is not None and inst.E * inst.E * inst.S <= 4e9:   # the reference's O(E^2 S) build (syn: ~2 min)
+                t = time.perf_counter()
+                h = R.problem(inst)
+                row["reference_problem_s"] = time.perf_counter() - t
+                del h
+            del dp
+        out[name] = row
+        print(name, json.dumps(row), flush=True)
+    if len(sys.argv) > 1:
+        pathlib.Path(sys.argv[1]).write_text(json.dumps(out, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()
