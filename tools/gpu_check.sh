@@ -34,11 +34,11 @@ for s in $STEPS; do
     ls)    run bench_ls 600 python -u tools/bench_ls.py --pop 4096 --steps 200 ;;
     ls1000) run bench_ls1000 600 python -u tools/bench_ls.py --pop 4096 --steps 1000 --cpu-sample 256 ;;
     listpmc) run listpmc 120 rocprofv3 -L ;;
-    pmc1)  run pmc1 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS --output-format csv -d "$OUT/pmc1" -o pmc -- python -u bench.py --no-cpu --steps 3 --warmup 1 ;;
-    pmc2)  run pmc2 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc2" -o pmc -- python -u bench.py --no-cpu --steps 3 --warmup 1 ;;
-    pmc3)  run pmc3 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc3" -o pmc -- python -u bench.py --no-cpu --steps 3 --warmup 1 ;;
-    pmc4)  run pmc4 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc4" -o pmc -- python -u bench.py --no-cpu --steps 3 --warmup 1 ;;
-    prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python -u bench.py --no-cpu --steps 100 ;;
+    pmc1)  run pmc1 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS --output-format csv -d "$OUT/pmc1" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
+    pmc2)  run pmc2 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc2" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
+    pmc3)  run pmc3 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc3" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
+    pmc4)  run pmc4 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc4" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
+    prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python -u bench.py --no-pmc --no-cpu --steps 100 ;;
   esac
 done
 echo "done"
