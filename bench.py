@@ -36,9 +36,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 POP_PER_GPU = 65536
 SIZE_NAMES = {"sm": "small01-size", "med": "medium01-size", "lg": "large01-size",
               "syn": "synthetic 2000/40/10/5000 scaling instance"}
-KERNELS = {1: "eval_tile", 2: "eval_block", 3: "eval_tile4", 4: "eval_tile4_w8", 5: "eval_tile5_alias",
-           6: "eval_tile5_alias_w8", 7: "eval_tile5", 8: "eval_tile5_w8",
-           9: "eval_lanes_w8+eval_waves", 10: "eval_lanes+eval_waves", 13: "eval_lanes_w16+eval_wide"}
+KERNELS = {2: "eval_block", 7: "eval_tile5", 8: "eval_tile5_w8", 13: "eval_lanes_w16+eval_corr"}
 
 
 def parse():
@@ -48,7 +46,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--pop", type=int, default=POP_PER_GPU)
     ap.add_argument("--config", default="med", choices=["sm", "med", "lg", "syn"])
-    ap.add_argument("--variant", type=int, default=0, help="tt_eval kernel: 0 auto, 1 lanes, 2 block")
+    ap.add_argument("--variant", type=int, default=0, help="tt_eval kernel: 0 auto, 2 block, 7/8 tile5, 13 wide path")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="individuals in the CPU-baseline sample (0: sized to about --cpu-seconds of CPU work)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)

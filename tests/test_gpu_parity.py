@@ -13,9 +13,8 @@ torch = pytest.importorskip("torch")
 from ttga import native  # noqa: E402
 
 NAMES = ["sm", "med", "tight"]
-# tt_eval kernels: 1 eval_tile, 2 eval_block, 3/4 eval_tile4 (4/8 waves), 5-8 eval_tile5, 9/10 split,
-# 13 wide path (eval_lanes<16> + eval_wide)
-EVAL_VARIANTS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13]
+# tt_eval kernels: 2 eval_block, 7/8 eval_tile5 (4/8 waves), 13 wide path (eval_lanes<16> + eval_corr)
+EVAL_VARIANTS = [2, 7, 8, 13]
 
 
 def load(golden_dir, name):
@@ -95,8 +94,9 @@ def test_eval_random_vs_oracle(orc, variant, dims):
 def test_eval_wide_vs_oracle(orc, dims):
     """Instances beyond eval_tile5 (E > 448): the wide path (variant 13, the
     automatic choice there) and the workgroup kernel against the oracle; E not a
-    multiple of 4 (byte row loads), R = 64 (full room masks), the largest E the
-    wide path takes, and the first E past eval_tile5."""
+    multiple of 4 (byte row loads), R = 64 (full room masks), E = 2430 (more
+    chunk pairs than waves: eval_corr reloads its words per round), and the
+    first E past eval_tile5."""
     inst = ttga.generate(*dims, seed=13)
     dp = native.DeviceProblem(inst)
     assert dp.eval_variant() == 13
@@ -109,8 +109,7 @@ def test_eval_wide_vs_oracle(orc, dims):
     slots[5, inst.E - 1] = 45                          # invalid gene in the last (partial) chunk: sentinels
     exp[0][5] = exp[1][5] = exp[3][5] = -1
     exp[2][5] = 0
-    variants = [2, 13] + ([1] if inst.E <= 1024 else [])
-    for v in variants:
+    for v in (2, 13):
         got = [host(t) for t in dp.eval(dev(slots), dev(rooms), variant=v)]
         for g, e in zip(got, exp):
             assert np.array_equal(g, e), v
@@ -135,8 +134,8 @@ def test_eval_empty_population(problems):
 
 
 def test_eval_bench_size_properties(orc):
-    """P = 65536 on the headline instance: the two independent kernels agree on
-    every individual, a strided sample matches the oracle, and feasibility
+    """P = 65536 on the headline instance: the eval kernels (tile5, the wide
+    path, the workgroup kernel) agree on every individual, a strided sample matches the oracle, and feasibility
     <=> hcv == 0 with penalty = feasible ? scv : 1e6 + hcv."""
     inst = ttga.config_instance("med")
     dp = native.DeviceProblem(inst)
@@ -144,8 +143,8 @@ def test_eval_bench_size_properties(orc):
     g = torch.Generator(device="cuda").manual_seed(0)
     slot = torch.randint(0, 45, (P, inst.E), dtype=torch.uint8, device="cuda", generator=g)
     room = dp.assign_rooms(slot)
-    a = [host(t) for t in dp.eval(slot, room, variant=3)]
-    for v in (v for v in EVAL_VARIANTS if v != 3):
+    a = [host(t) for t in dp.eval(slot, room, variant=8)]
+    for v in (v for v in EVAL_VARIANTS if v != 8):
         b = [host(t) for t in dp.eval(slot, room, variant=v)]
         for x, y in zip(a, b):
             assert np.array_equal(x, y)

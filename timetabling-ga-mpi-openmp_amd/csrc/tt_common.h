@@ -9,7 +9,6 @@ constexpr int kSlots = 45;             // Solution.cpp:52,57
 constexpr int kSlotsPerDay = 9;
 constexpr int kMaxRooms = 64;          // rooms are bitmasks in one 64-bit word
 constexpr int kMaxSlotEvents = 256;    // per-slot event bitsets (4 x 64 bits) in the matcher
-constexpr int kTileWaves = 8;          // waves per workgroup of the eval tile kernel
 
 // slot s is the last of its day (s % 9 == 8): Solution.cpp:94
 constexpr uint64_t kLastSlotMask = (1ull << 8) | (1ull << 17) | (1ull << 26) | (1ull << 35) | (1ull << 44);
@@ -26,19 +25,14 @@ struct DevProblem {
     const int32_t* ev_stu;        //   students of each event, ascending
     const uint64_t* poss;         // [E] possibleRooms as room bitmasks
     const uint32_t* corr;         // [E*EW] eventCorrelations bit-matrix (diagonal included)
-    const int32_t* cp_off;        // [E+1] upper-triangle correlation lists (j > i)
-    const int32_t* cp_j;
     int EW64;                     // 64-bit words per event bitset
     const uint64_t* cupT;         // [EW64][E] upper-triangle correlation bits, word-major:
                                   //   cupT[w*E+i] bit b <=> corr(i, 64w+b) and 64w+b > i
     const uint64_t* corr64;       // [E][EW64] full eventCorrelations rows (diagonal included)
-    const uint4* wch;             // lane-phase chunk stream of the tile kernel: 8 u16 event ids
-                                  //   per record, students s = w mod kTileWaves for wave w,
-                                  //   bit 15 of id 0 = last chunk of a student (E <= 32767)
-    const int32_t* wch_off;       // [kTileWaves+1] record offsets per wave
     const int32_t* stc_off;       // [S+1] per-student event lists padded to multiples of 8
     const int32_t* stc_ev;        //   padding entries hold E (a sentinel column)
-    const uint4* sch;             // the same records in student order (eval_tile4)
+    const uint4* sch;             // lane-phase records in student order: 8 u16 event ids (the
+                                  //   stc lists), bit 15 of id 0 = last record of a student
     const int32_t* sch_part;      // record offsets of each wave's contiguous student range:
                                   //   [kSchPart4 + w] for 4-wave, [kSchPart8 + w] for 8-wave and
                                   //   [kSchPart16 + w] for 16-wave groups

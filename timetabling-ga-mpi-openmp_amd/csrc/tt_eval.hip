@@ -13,483 +13,58 @@
 //       + #{e : room_e not possible for e};
 //   feasible <=> hcv == 0 (Solution.cpp:63-84 tests the same three conditions).
 //
-// Two kernels:
-//  * eval_tile (E <= 1024): one workgroup per tile of 64 individuals, mixing a
-//    lane-per-individual phase (attendance masks) with a wave-per-individual
-//    phase (bitset hcv terms); see below.
-//  * eval_block (any E): one 256-thread workgroup per individual; slot
-//    buckets in LDS enumerate only same-slot pairs for the correlation term.
+// Kernels (tt_eval_variant numbering):
+//  *  8 / 7  eval_tile5 (E <= 448; 8 / 4 waves): one workgroup per tile of 64
+//            individuals, a lane-per-individual phase (attendance masks) and a
+//            wave-per-individual phase (bitset hcv terms) with the upper-triangle
+//            correlation words resident in registers;
+//  * 13      the wide path (E > 448): eval_lanes (the lane phase over a 64-row
+//            tile, 16 waves) + eval_corr (the hcv terms for batches of
+//            individuals; each wave keeps the correlation words of a pair of
+//            64-event chunks in registers for the whole launch);
+//  *  2      eval_block (any E): one 256-thread workgroup per individual.
 #include <algorithm>
 #include <type_traits>
+#include <utility>
 
 #include "tt_internal.h"
 
 namespace ttga {
 
-// ---------------------------------------------------------------- eval_tile
-// One workgroup of kTileWaves waves per tile of 64 individuals (persistent
-// over tiles). The tile's slot rows sit in LDS with an odd-dword row stride
-// plus a sentinel column E (slot 63, outside every day mask).
-//  * lane phase (LANE = INDIVIDUAL): wave w builds the 45-bit attendance mask
-//    of students w, w+8, ... from 8-padded event lists (8 independent
-//    conflict-free ds_read_u8 per chunk) -> >2-in-a-row and single-class terms;
-//  * wave phase (WAVE = INDIVIDUAL): per-slot event bitsets B[t] (ds_or_b64),
-//    room-cell counters (ds_add_rtn), unsuitable rooms, last-slot term, and the
-//    correlated same-slot pairs as popcount(cupT[w][i] & B[slot_i][w]) over the
-//    upper-triangle words (1.6 K word ops per individual at E=400 instead of
-//    13 K neighbour lookups).
-
-
-struct TileLayout {
-    int SP;           // tile row stride (bytes)
-    int WS;           // per-wave scratch bytes
-    size_t off_wave;  // start of per-wave scratch
-    size_t off_part;  // [kTileWaves][64] lane-phase partials, then hq[64], sq[64]
-    size_t bytes;
-};
-
-__host__ __device__ inline TileLayout tile_layout(int E, int R) {
-    TileLayout L;
-    int sp = (E + 1 + 3) & ~3;                 // room for the sentinel column
-    if (((sp >> 2) & 1) == 0) sp += 4;         // odd dword stride: conflict-free column reads
-    L.SP = sp;
-    const int ew64 = (E + 63) / 64;
-    L.WS = (kSlots * ew64 * 8 + kSlots * R * 4 + 15) & ~15;
-    L.off_wave = ((size_t)64 * sp + 15) & ~(size_t)15;
-    L.off_part = L.off_wave + (size_t)kTileWaves * L.WS;
-    L.bytes = L.off_part + 4 * (size_t)(kTileWaves * 64 + 128);
-    return L;
-}
-
-// EWC > 0: compile-time number of 64-event words (E <= 64*EWC); the per-event
-// invariants of a lane's events (possible rooms, studentNumber, the upper-
-// triangle correlation words) live in registers for the whole launch, so an
-// individual costs only its own slot/room reads plus LDS traffic.
-// EWC == 0: runtime word count, invariants re-read from global memory.
-template <int EWC>
-__global__ __launch_bounds__(64 * kTileWaves) void eval_tile_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
-                                                                     const uint8_t* __restrict__ room, int P,
-                                                                     int32_t* __restrict__ hcv_out,
-                                                                     int32_t* __restrict__ scv_out,
-                                                                     uint8_t* __restrict__ feas_out,
-                                                                     int32_t* __restrict__ pen_out, int ablate) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int E = pb.E, R = pb.R;
-    const int EW64 = EWC > 0 ? EWC : pb.EW64;
-    const int lane = threadIdx.x & 63, wv = wave_id();
-    const TileLayout L = tile_layout(E, R);
-    // ablate (profiling only, results invalid): 1 skip lane phase, 2 skip wave phase, 4 skip corr words
-    const int SP = L.SP;
-    uint8_t* tile = lds;
-    uint64_t* B = (uint64_t*)(lds + L.off_wave + (size_t)wv * L.WS);   // [45][EW64]
-    uint32_t* cnt = (uint32_t*)(B + kSlots * EW64);                     // [45*R]
-    int32_t* part = (int32_t*)(lds + L.off_part);                       // [kTileWaves][64]
-    int32_t* hq = part + kTileWaves * 64;                               // [64]
-    int32_t* sq = hq + 64;                                              // [64]
-    const int tiles = (P + 63) / 64;
-    const int nthr = 64 * kTileWaves;
-
-    constexpr int NR = EWC > 0 ? EWC : 1;
-    uint64_t inv_poss[NR], inv_cup[NR][NR];
-    int inv_sn[NR];
-    if constexpr (EWC > 0) {
-#pragma unroll
-        for (int r = 0; r < EWC; ++r) {
-            const int e = lane + 64 * r;
-            const bool ok = e < E;
-            inv_poss[r] = ok ? pb.poss[e] : ~0ull;
-            inv_sn[r] = ok ? pb.sn[e] : 0;
-#pragma unroll
-            for (int w = 0; w < EWC; ++w) inv_cup[r][w] = (w >= r && ok) ? pb.cupT[(size_t)w * E + e] : 0ull;
-        }
-    }
-
-    for (int tl = blockIdx.x; tl < tiles; tl += gridDim.x) {
-        const long p0 = (long)tl * 64;
-        const int np = (int)min((long)64, (long)P - p0);
-        __syncthreads();
-        // ---- stage slot rows + sentinel column
-        const uint8_t* src = slot + p0 * E;
-        if ((E & 3) == 0) {
-            const int wpr = E >> 2;
-            const uint32_t* s32 = (const uint32_t*)src;
-            for (int w = threadIdx.x; w < np * wpr; w += nthr) {
-                const int r = w / wpr, c = w - r * wpr;
-                *(uint32_t*)(tile + r * SP + 4 * c) = s32[w];
-            }
-        } else {
-            for (int b = threadIdx.x; b < np * E; b += nthr) {
-                const int r = b / E, c = b - r * E;
-                tile[r * SP + c] = src[b];
-            }
-        }
-        if (threadIdx.x < 64) tile[threadIdx.x * SP + E] = 63;
-        __syncthreads();
-
-        // ---- lane phase: per-student attendance masks (Solution.cpp:98-137)
-        if (!(ablate & 1)) {
-            // this wave's students as one stream of 8-id chunk records; the next
-            // record is loaded while the current one's 8 LDS reads are in flight
-            const uint8_t* my = tile + lane * SP;
-            int sc = 0;
-            const int c0 = pb.wch_off[wv], c1 = pb.wch_off[wv + 1];
-            if (c0 < c1) {
-                uint4 cur = pb.wch[c0];
-                uint64_t m = 0;
-                for (int c = c0; c < c1; ++c) {
-                    const uint4 nxt = pb.wch[c + 1 < c1 ? c + 1 : c];
-                    const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
-                    uint32_t sl[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) sl[j] = my[(w[j >> 1] >> (16 * (j & 1))) & 0x7FFFu];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) m |= 1ull << (sl[j] & 63);
-                    if (cur.x & 0x8000u) {                       // last chunk of a student
-                        sc += __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);
-#pragma unroll
-                        for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);
-                        m = 0;
-                    }
-                    cur = nxt;
-                }
-            }
-            part[wv * 64 + lane] = sc;
-        }
-
-        // ---- wave phase: hcv terms + last-slot term, one individual per wave at a time
-        for (int q = wv; q < ((ablate & 2) ? 0 : np); q += kTileWaves) {
-            for (int c = lane; c < kSlots * EW64; c += 64) B[c] = 0ull;
-            for (int c = lane; c < kSlots * R; c += 64) cnt[c] = 0u;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint8_t* rs = tile + q * SP;
-            const uint8_t* rr = room + (p0 + q) * E;
-            int h = 0, last = 0;
-            bool bad = false;
-            if constexpr (EWC > 0) {
-                uint32_t sv[EWC], rv[EWC];
-#pragma unroll
-                for (int r = 0; r < EWC; ++r) {
-                    const int e = lane + 64 * r;
-                    sv[r] = e < E ? rs[e] : 0u;
-                    rv[r] = e < E ? rr[e] : 0u;
-                }
-#pragma unroll
-                for (int r = 0; r < EWC; ++r) {
-                    if (lane + 64 * r < E) {
-                        const int s = sv[r], ro = rv[r];
-                        if (s >= kSlots || ro >= R) {
-                            bad = true;
-                        } else {
-                            atomicOr((unsigned long long*)&B[s * EWC + r], 1ull << lane);
-                            h += (int)atomicAdd(&cnt[s * R + ro], 1u);                 // Solution.cpp:148-150
-                            h += (int)(((inv_poss[r] >> ro) & 1ull) ^ 1ull);            // :155-156
-                            last += inv_sn[r] * (int)((kLastSlotMask >> s) & 1ull);     // :93-96
-                        }
-                    }
-                }
-                const bool any_bad = __any(bad);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (!any_bad && !(ablate & 4)) {
-#pragma unroll
-                    for (int r = 0; r < EWC; ++r) {                                     // :151-153
-                        if (lane + 64 * r < E) {
-                            const uint64_t* brow = B + sv[r] * EWC;
-#pragma unroll
-                            for (int w = r; w < EWC; ++w) h += __popcll(inv_cup[r][w] & brow[w]);
-                        }
-                    }
-                }
-                bad = any_bad;
-            } else {
-                for (int e = lane; e < E; e += 64) {
-                    const int s = rs[e], r = rr[e];
-                    if (s >= kSlots || r >= R) { bad = true; continue; }
-                    atomicOr((unsigned long long*)&B[s * EW64 + (e >> 6)], 1ull << (e & 63));
-                    h += (int)atomicAdd(&cnt[s * R + r], 1u);
-                    h += (int)(((pb.poss[e] >> r) & 1ull) ^ 1ull);
-                    last += pb.sn[e] * (int)((kLastSlotMask >> s) & 1ull);
-                }
-                const bool any_bad = __any(bad);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (!any_bad && !(ablate & 4)) {
-                    for (int i = lane; i < E; i += 64) {
-                        const uint64_t* brow = B + rs[i] * EW64;
-                        for (int w = i >> 6; w < EW64; ++w) h += __popcll(pb.cupT[(size_t)w * E + i] & brow[w]);
-                    }
-                }
-                bad = any_bad;
-            }
-            h = wave_sum(h);
-            last = wave_sum(last);
-            if (lane == 0) { hq[q] = bad ? -1 : h; sq[q] = last; }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        __syncthreads();
-        if (wv == 0 && lane < np) {
-            const long p = p0 + lane;
-            const int h = hq[lane];
-            if (h < 0) {
-                hcv_out[p] = -1; scv_out[p] = -1; feas_out[p] = 0; pen_out[p] = -1;
-            } else {
-                int sc = sq[lane];
-#pragma unroll
-                for (int w = 0; w < kTileWaves; ++w) sc += part[w * 64 + lane];
-                hcv_out[p] = h;
-                scv_out[p] = sc;
-                feas_out[p] = h == 0 ? 1 : 0;
-                pen_out[p] = h == 0 ? sc : 1000000 + h;
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------- eval_tile4
-// Second-generation tile kernel: NW waves per 64-individual tile, sized so that
-// at E = 400 four workgroups (16 waves) fit one CU and a 65,536-member
-// population is one tile per workgroup.
-//  * lane-phase records come through the scalar cache (s_load_dwordx4 via the
-//    constant address space) from a student-ordered stream; wave w owns a
-//    contiguous student range balanced by record count;
-//  * the wave phase prefetches the next individual's room row while the
-//    current one is scored; cell counters are packed u16 pairs;
-//  * PK selects how a lane keeps possibleRooms/studentNumber of its events:
-//    1 = one packed register (R <= 16, studentNumber < 65536), 2 = u32 mask
-//    (R <= 32), 0 = u64 mask.
 typedef __attribute__((address_space(4))) const uint32_t ConstU32;
 typedef __attribute__((address_space(4))) const int32_t ConstI32;
 
-struct Tile4Layout {
-    int SP, WS;
-    size_t off_wave, off_part, bytes;
-};
-
-__host__ __device__ inline Tile4Layout tile4_layout(int E, int R, int NW) {
-    Tile4Layout L;
-    int sp = (E + 1 + 3) & ~3;
-    if (((sp >> 2) & 1) == 0) sp += 4;
-    L.SP = sp;
-    const int ew64 = (E + 63) / 64;
-    const int cntw = (kSlots * R + 1) / 2;
-    L.WS = (kSlots * ew64 * 8 + cntw * 4 + 15) & ~15;
-    L.off_wave = ((size_t)64 * sp + 15) & ~(size_t)15;
-    L.off_part = L.off_wave + (size_t)NW * L.WS;
-    L.bytes = L.off_part + 4 * (size_t)(NW * 64 + 64);
-    return L;
-}
-
-template <int EWC, int NW, int PK>
-__global__ __launch_bounds__(64 * NW, 16 / NW) void eval_tile4_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
-                                                              const uint8_t* __restrict__ room, int P,
-                                                              int32_t* __restrict__ hcv_out,
-                                                              int32_t* __restrict__ scv_out,
-                                                              uint8_t* __restrict__ feas_out,
-                                                              int32_t* __restrict__ pen_out, int ablate) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    constexpr int NT = 64 * NW;
-    const int E = pb.E, R = pb.R;
-    const int lane = threadIdx.x & 63, wv = wave_id();
-    const Tile4Layout L = tile4_layout(E, R, NW);
-    const int SP = L.SP;
-    uint8_t* tile = lds;
-    uint8_t* ws = lds + L.off_wave + (size_t)wv * L.WS;
-    uint64_t* B = (uint64_t*)ws;                              // [45][EWC] event bitsets per slot
-    uint32_t* cnt = (uint32_t*)(B + kSlots * EWC);            // [45*R] u16 cell counters, 2 per dword
-    int32_t* part = (int32_t*)(lds + L.off_part);             // [NW][64] scv partials
-    int32_t* hq = part + NW * 64;                             // [64] hcv (or -1)
-    const int tiles = (P + 63) / 64;
-
-    // per-event invariants of this lane's events e = lane + 64 r
-    using PossT = typename std::conditional<PK == 0, uint64_t, uint32_t>::type;
-    uint64_t inv_cup[EWC][EWC];
-    PossT inv_poss[EWC];
-    uint32_t inv_ps[EWC];
-    int inv_sn[EWC];
-#pragma unroll
-    for (int r = 0; r < EWC; ++r) {
-        const int e = lane + 64 * r;
-        const bool ok = e < E;
-        if constexpr (PK == 1) {
-            inv_ps[r] = ok ? ((uint32_t)pb.poss[e] | ((uint32_t)pb.sn[e] << 16)) : 0xFFFFu;
-        } else {
-            inv_poss[r] = ok ? (PossT)pb.poss[e] : (PossT)~0ull;
-            inv_sn[r] = ok ? pb.sn[e] : 0;
-        }
-#pragma unroll
-        for (int w = 0; w < EWC; ++w) inv_cup[r][w] = (w >= r && ok) ? pb.cupT[(size_t)w * E + e] : 0ull;
-    }
-    const ConstU32* rec = (const ConstU32*)pb.sch;
-    const ConstI32* ptab = (const ConstI32*)pb.sch_part;
-    const int pbase = NW == 4 ? kSchPart4 : kSchPart8;
-    const int c0 = ptab[pbase + wv], c1 = ptab[pbase + wv + 1];
-    const bool wide = (E & 15) == 0 && (((uintptr_t)slot) & 15) == 0;
-    const int qpr = E >> 4;
-    const uint32_t qinv = ((1u << 20) + (uint32_t)qpr - 1) / (uint32_t)max(qpr, 1);   // w / qpr for w < 2^12
-
-    for (int tl = blockIdx.x; tl < tiles; tl += gridDim.x) {
-        const long p0 = (long)tl * 64;
-        const int np = (int)min((long)64, (long)P - p0);
-        __syncthreads();
-        // ---- stage the tile's slot rows (+ sentinel column E = slot 63)
-        const uint8_t* src = slot + p0 * E;
-        if (wide) {
-            const uint4* s16 = (const uint4*)src;
-#pragma unroll 2
-            for (int w = threadIdx.x; w < np * qpr; w += NT) {
-                const int r = (int)(((uint32_t)w * qinv) >> 20), c = w - r * qpr;
-                const uint4 v = s16[w];
-                uint32_t* d = (uint32_t*)(tile + r * SP + 16 * c);
-                d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-            }
-        } else {
-#pragma unroll 1
-            for (int r = wv; r < np; r += NW)
-#pragma unroll 1
-                for (int c = lane; c < E; c += 64) tile[r * SP + c] = src[(long)r * E + c];
-        }
-        if (threadIdx.x < 64) tile[threadIdx.x * SP + E] = 63;
-        __syncthreads();
-
-        // ---- lane phase (lane = individual): attendance masks of this wave's students
-        int sc = 0;
-        if (!(ablate & 1) && c0 < c1) {
-            const uint8_t* my = tile + lane * SP;
-            uint32_t cur[4] = {rec[4 * c0], rec[4 * c0 + 1], rec[4 * c0 + 2], rec[4 * c0 + 3]};
-            uint64_t m = 0;
-            for (int c = c0; c < c1; ++c) {
-                const int cn = c + 1 < c1 ? c + 1 : c;
-                const uint32_t nxt[4] = {rec[4 * cn], rec[4 * cn + 1], rec[4 * cn + 2], rec[4 * cn + 3]};
-                const uint32_t* w = cur;
-                uint32_t sl[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) sl[j] = my[(w[j >> 1] >> (16 * (j & 1))) & 0x7FFFu];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) m |= 1ull << (sl[j] & 63);
-                if (cur[0] & 0x8000u) {                                  // last record of a student
-                    sc += __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);   // Solution.cpp:99-117
-#pragma unroll
-                    for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);   // :119-137
-                    m = 0;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
-            }
-        }
-        part[wv * 64 + lane] = sc;
-
-        // ---- wave phase (wave = individual): hcv terms + last-slot term
-        const int nq = (ablate & 2) ? 0 : np;
-        uint32_t rvn[EWC];
-#pragma unroll
-        for (int r = 0; r < EWC; ++r) rvn[r] = 0u;
-        if (wv < nq) {
-            const uint8_t* rr = room + (p0 + wv) * E;
-#pragma unroll
-            for (int r = 0; r < EWC; ++r) rvn[r] = lane + 64 * r < E ? rr[lane + 64 * r] : 0u;
-        }
-        for (int q = wv; q < nq; q += NW) {
-            uint32_t rv[EWC], sv[EWC];
-#pragma unroll
-            for (int r = 0; r < EWC; ++r) rv[r] = rvn[r];
-            if (q + NW < nq) {                                          // prefetch the next room row
-                const uint8_t* rr = room + (p0 + q + NW) * E;
-#pragma unroll
-                for (int r = 0; r < EWC; ++r) rvn[r] = lane + 64 * r < E ? rr[lane + 64 * r] : 0u;
-            }
-            for (int c = lane; c < (L.WS >> 4); c += 64) ((uint4*)ws)[c] = make_uint4(0u, 0u, 0u, 0u);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint8_t* rs = tile + q * SP;
-#pragma unroll
-            for (int r = 0; r < EWC; ++r) sv[r] = lane + 64 * r < E ? rs[lane + 64 * r] : 0u;
-            int h = 0, last = 0;
-            bool bad = false;
-#pragma unroll
-            for (int r = 0; r < EWC; ++r) {
-                if (lane + 64 * r < E) {
-                    const uint32_t s = sv[r], ro = rv[r];
-                    if (s >= (uint32_t)kSlots || ro >= (uint32_t)R) {
-                        bad = true;
-                    } else {
-                        atomicOr((unsigned long long*)&B[s * EWC + r], 1ull << lane);
-                        const uint32_t cell = s * R + ro, sh = (cell & 1u) << 4;
-                        const uint32_t old = atomicAdd(&cnt[cell >> 1], 1u << sh);
-                        h += (int)((old >> sh) & 0xFFFFu);                               // Solution.cpp:148-150
-                        const bool last_slot = (kLastSlotMask >> s) & 1ull;
-                        if constexpr (PK == 1) {
-                            h += (int)(((inv_ps[r] >> ro) & 1u) ^ 1u);                  // :155-156
-                            last += last_slot ? (int)(inv_ps[r] >> 16) : 0;             // :93-96
-                        } else {
-                            h += (int)(((inv_poss[r] >> ro) & 1u) ^ 1u);
-                            last += last_slot ? inv_sn[r] : 0;
-                        }
-                    }
-                }
-            }
-            const bool any_bad = __any(bad);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (!any_bad && !(ablate & 4)) {
-#pragma unroll
-                for (int r = 0; r < EWC; ++r) {                                         // :151-153
-                    if (lane + 64 * r < E) {
-                        const uint64_t* brow = B + sv[r] * EWC;
-#pragma unroll
-                        for (int w = r; w < EWC; ++w) h += __popcll(inv_cup[r][w] & brow[w]);
-                    }
-                    if (r & 1) __builtin_amdgcn_sched_barrier(0);   // bound the B words in flight (VGPRs)
-                }
-            }
-            h = wave_sum(h);
-            last = wave_sum(last);
-            if (lane == 0) {
-                hq[q] = any_bad ? -1 : h;
-                part[wv * 64 + q] += last;
-            }
-        }
-        __syncthreads();
-        if (wv == 0 && lane < np) {
-            const long p = p0 + lane;
-            const int h = hq[lane];
-            if (h < 0) {
-                hcv_out[p] = -1; scv_out[p] = -1; feas_out[p] = 0; pen_out[p] = -1;
-            } else {
-                int s2 = 0;
-#pragma unroll
-                for (int w = 0; w < NW; ++w) s2 += part[w * 64 + lane];
-                hcv_out[p] = h;
-                scv_out[p] = s2;
-                feas_out[p] = h == 0 ? 1 : 0;
-                pen_out[p] = h == 0 ? s2 : 1000000 + h;
-            }
-        }
-    }
-}
-
 // ---------------------------------------------------------------- eval_tile5
-// Third-generation tile kernel. Same two phases as eval_tile4, rearranged so
-// that the LDS holds either the tile or the wave workspaces, never both:
-//  * lane phase as eval_tile4 (8-padded per-student records through the scalar
-//    cache; a back-to-back record stream with per-entry end flags measured
-//    slower: its uniform per-entry branches serialise the mask updates);
-//  * after a workgroup barrier the tile is dead and its bytes become the
-//    per-wave workspaces; the wave phase reads each individual's slot and
-//    room rows straight from global memory (L2-hot: the staging loads just
-//    touched them), one individual ahead;
+// NW waves per 64-individual tile, persistent over tiles.
+//  * lane phase (LANE = INDIVIDUAL): per-student records of 8 u16 event ids
+//    (padded with the sentinel column E = slot 63, end-of-student flag in bit
+//    15) come through the scalar cache (s_load_dwordx4 via the constant
+//    address space) from a student-ordered stream; wave w owns a contiguous
+//    student range balanced by record count; 8 conflict-free ds_read_u8 per
+//    record from the tile (odd-dword row stride) build the 45-bit attendance
+//    mask -> >2-in-a-row and single-class terms. A back-to-back record stream
+//    with per-entry end flags measured slower: its uniform per-entry branches
+//    serialise the mask updates;
+//  * wave phase (WAVE = INDIVIDUAL): slot rows from the tile, room rows from
+//    global memory one individual ahead; per-slot event bitsets B[t]
+//    (ds_or_b64), room-cell counters (packed u16, ds_add_rtn), unsuitable
+//    rooms, last-slot term, and the correlated same-slot pairs as
+//    popcount(cupT[w][i] & B[slot_i][w]) over the upper-triangle words, which
+//    (with possibleRooms and studentNumber) stay in registers for the launch;
 //  * an individual with an invalid gene is detected from registers before any
-//    LDS work (its outputs are the -1 sentinels anyway); the valid path has
-//    no per-event branches except on the last, partial event word;
-//  * CNT32: u32 cell counters (address = one mad); otherwise packed u16 pairs;
-//  * B rows are read with single ds_read_b64 (lds_row_b64 below).
+//    LDS work (its outputs are the -1 sentinels); the valid path has no
+//    per-event branches except on the last, partial event word;
+//  * PK: 1 = possibleRooms | studentNumber << 16 in one register (R <= 16,
+//    studentNumber < 65536), 2 = u32 mask (R <= 32), 0 = u64 mask.
+
+// acc + popcount(x) as two v_bcnt_u32_b32 with accumulate (no separate add).
+// (The compiler turns the plain form into bcnt, bcnt, add3.)
+__device__ __forceinline__ int popc_acc(uint64_t x, int acc) {
+    int r, t;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(t) : "v"((uint32_t)x), "v"(acc));
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"((uint32_t)(x >> 32)), "v"(t));
+    return r;
+}
 
 // LDS byte address of a pointer into dynamic shared memory.
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
@@ -538,10 +113,93 @@ __device__ __forceinline__ void corr_words(uint32_t bbase, const uint32_t* sv, c
             uint64_t bw[EWC - R];
             lds_row_b64<EWC - R>(bbase + sv[R] * (uint32_t)(EWC * 8) + 8 * R, bw);
 #pragma unroll
-            for (int w = R; w < EWC; ++w) h += __popcll(cup[R][w] & bw[w - R]);
+            for (int w = R; w < EWC; ++w) h = popc_acc(cup[R][w] & bw[w - R], h);
         }
         corr_words<R + 1, EWC>(bbase, sv, cup, lane, E, last_partial, h);
     }
+}
+
+// ---------------------------------------------------------------- lane loop
+// Attendance masks of students whose records c0..c1-1 (8 u16 event ids each,
+// sentinel column E = slot 63, bit 15 of id 0 = the student's last record)
+// this wave owns; lane = individual, `my` = its tile row. Returns the lane's
+// >2-in-a-row + single-class count (Solution.cpp:99-137). U = 1: one record
+// per step, the next record's scalar load issued with it; U = kLanePF: four
+// records per step with the next step's records prefetched (eval_lanes; on
+// the medium instance the plain form is faster inside eval_tile5).
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+// 16 dwords through the scalar cache, issued now, waited for by sld_wait
+// (the compiler does not track this load: every use goes through sld_wait,
+// whose "+s" makes the registers depend on the wait).
+__device__ __forceinline__ u32x16 sload16(const uint32_t* p) {
+    u32x16 v;
+    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ void sld_wait(u32x16& v) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v) : : "memory"); }
+
+constexpr int kLanePF = 4;     // lane_scv mode: 4 records per step with scalar prefetch
+
+template <int U>
+__device__ __forceinline__ int lane_scv(const uint8_t* my, const ConstU32* rec, int c0, int c1) {
+    int sc = 0;
+    uint64_t m = 0;
+    auto fin = [&]() {
+        sc += __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);                          // :99-117
+#pragma unroll
+        for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);   // :119-137
+        m = 0;
+    };
+    int c = c0;
+    if constexpr (U == kLanePF) {
+        // 4 records (one s_load_dwordx16) per step, the next step's records in
+        // flight while this step's 32 ds_read_u8 run: waited for (lgkmcnt(0))
+        // at the top of the next step, so the record stream's scalar-cache
+        // misses overlap the LDS work instead of stalling every step.
+        auto step = [&](const u32x16& r) {
+            uint32_t sl[32];
+#pragma unroll
+            for (int j = 0; j < 32; ++j) sl[j] = my[(r[j >> 1] >> (16 * (j & 1))) & 0x7FFFu];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) m |= 1ull << (sl[8 * u + j] & 63);
+                if (r[4 * u] & 0x8000u) fin();
+            }
+        };
+        // ping-pong registers (no copy of a register still being loaded)
+        if (c + 4 <= c1) {
+            u32x16 ra = sload16((const uint32_t*)(rec + 4 * c)), rb;
+            while (true) {
+                sld_wait(ra);
+                rb = sload16((const uint32_t*)(rec + 4 * (c + 8 <= c1 ? c + 4 : c)));
+                step(ra);
+                c += 4;
+                if (c + 4 > c1) { sld_wait(rb); break; }
+                sld_wait(rb);
+                ra = sload16((const uint32_t*)(rec + 4 * (c + 8 <= c1 ? c + 4 : c)));
+                step(rb);
+                c += 4;
+                if (c + 4 > c1) { sld_wait(ra); break; }
+            }
+        }
+    }
+    if (c < c1) {
+        uint32_t cur[4] = {rec[4 * c], rec[4 * c + 1], rec[4 * c + 2], rec[4 * c + 3]};
+        for (; c < c1; ++c) {
+            const int cn = c + 1 < c1 ? c + 1 : c;
+            const uint32_t nxt[4] = {rec[4 * cn], rec[4 * cn + 1], rec[4 * cn + 2], rec[4 * cn + 3]};
+            uint32_t sl[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sl[j] = my[(cur[j >> 1] >> (16 * (j & 1))) & 0x7FFFu];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m |= 1ull << (sl[j] & 63);
+            if (cur[0] & 0x8000u) fin();
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+        }
+    }
+    return sc;
 }
 
 struct Tile5Layout {
@@ -549,22 +207,21 @@ struct Tile5Layout {
     size_t off_ws, off_part, bytes;
 };
 
-__host__ __device__ inline Tile5Layout tile5_layout(int E, int R, int NW, bool cnt32, bool alias) {
+__host__ __device__ inline Tile5Layout tile5_layout(int E, int R, int NW) {
     Tile5Layout L;
-    int sp = (E + 1 + 3) & ~3;
-    if (((sp >> 2) & 1) == 0) sp += 4;
+    int sp = (E + 1 + 3) & ~3;                 // room for the sentinel column
+    if (((sp >> 2) & 1) == 0) sp += 4;         // odd dword stride: conflict-free column reads
     L.SP = sp;
     const int ew64 = (E + 63) / 64;
-    const int cntb = cnt32 ? kSlots * R * 4 : ((kSlots * R + 1) / 2) * 4;
+    const int cntb = ((kSlots * R + 1) / 2) * 4;
     L.WS = (kSlots * ew64 * 8 + cntb + 15) & ~15;
-    L.off_ws = alias ? 0 : (((size_t)64 * sp + 15) & ~(size_t)15);
-    const size_t uni = alias ? std::max((size_t)64 * sp, (size_t)NW * L.WS) : L.off_ws + (size_t)NW * L.WS;
-    L.off_part = (uni + 15) & ~(size_t)15;
+    L.off_ws = ((size_t)64 * sp + 15) & ~(size_t)15;
+    L.off_part = L.off_ws + (size_t)NW * L.WS;
     L.bytes = L.off_part + 4 * (size_t)(NW * 64 + 64);
     return L;
 }
 
-template <int EWC, int NW, bool CNT32, int PK, bool ALIAS>
+template <int EWC, int NW, int PK, int U>
 __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
                                                               const uint8_t* __restrict__ room, int P,
                                                               int32_t* __restrict__ hcv_out,
@@ -575,19 +232,17 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
     constexpr int NT = 64 * NW;
     const int E = pb.E, R = pb.R;
     const int lane = threadIdx.x & 63, wv = wave_id();
-    const Tile5Layout L = tile5_layout(E, R, NW, CNT32, ALIAS);
+    const Tile5Layout L = tile5_layout(E, R, NW);
     const int SP = L.SP;
     uint8_t* tile = lds;
-    uint8_t* ws = lds + L.off_ws + (size_t)wv * L.WS;         // ALIAS: on top of the dead tile
+    uint8_t* ws = lds + L.off_ws + (size_t)wv * L.WS;
     uint64_t* B = (uint64_t*)ws;                              // [45][EWC] event bitsets per slot
-    uint32_t* cnt = (uint32_t*)(B + kSlots * EWC);            // cell counters
+    uint32_t* cnt = (uint32_t*)(B + kSlots * EWC);            // packed u16 cell counters
     int32_t* part = (int32_t*)(lds + L.off_part);             // [NW][64] scv partials
     int32_t* hq = part + NW * 64;                             // [64] hcv (or -1)
     const int tiles = (P + 63) / 64;
     const bool last_partial = E < 64 * EWC;                   // lanes of word EWC-1 beyond E
 
-    // PK as in eval_tile4: 1 = possibleRooms | studentNumber << 16 in one register
-    // (R <= 16, studentNumber < 65536), 2 = u32 mask (R <= 32), 0 = u64 mask
     using PossT = typename std::conditional<PK == 0, uint64_t, uint32_t>::type;
     uint64_t inv_cup[EWC][EWC];
     PossT inv_poss[EWC];
@@ -608,7 +263,7 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
     }
     const ConstU32* rec = (const ConstU32*)pb.sch;
     const ConstI32* ptab = (const ConstI32*)pb.sch_part;
-    const int pbase = NW == 4 ? kSchPart4 : kSchPart8;
+    const int pbase = sch_part_base(NW);
     const int c0 = ptab[pbase + wv], c1 = ptab[pbase + wv + 1];
     const bool wide = (E & 15) == 0 && (((uintptr_t)slot) & 15) == 0;
     const int qpr = E >> 4;
@@ -639,59 +294,28 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
         __syncthreads();
 
         // ---- lane phase (lane = individual): attendance masks of this wave's students
-        int sc = 0;
-        if (!(ablate & 1) && c0 < c1) {
-            const uint8_t* my = tile + lane * SP;
-            uint32_t cur[4] = {rec[4 * c0], rec[4 * c0 + 1], rec[4 * c0 + 2], rec[4 * c0 + 3]};
-            uint64_t m = 0;
-            for (int c = c0; c < c1; ++c) {
-                const int cn = c + 1 < c1 ? c + 1 : c;
-                const uint32_t nxt[4] = {rec[4 * cn], rec[4 * cn + 1], rec[4 * cn + 2], rec[4 * cn + 3]};
-                uint32_t sl[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) sl[j] = my[(cur[j >> 1] >> (16 * (j & 1))) & 0x7FFFu];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) m |= 1ull << (sl[j] & 63);
-                if (cur[0] & 0x8000u) {                                  // last record of a student
-                    sc += __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);   // Solution.cpp:99-117
-#pragma unroll
-                    for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);   // :119-137
-                    m = 0;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
-            }
-        }
+        const int sc = (!(ablate & 1) && c0 < c1) ? lane_scv<U>(tile + lane * SP, rec, c0, c1) : 0;
         part[wv * 64 + lane] = sc;
-        if constexpr (ALIAS) __syncthreads();                           // the tile is dead from here
 
         // ---- wave phase (wave = individual): hcv terms + last-slot term
         const int nq = (ablate & 2) ? 0 : np;
-        // one row (slot rows if ALIAS, else room rows) is prefetched one individual ahead
-        uint32_t pfn[EWC];
+        uint32_t pfn[EWC];                                        // room row, one individual ahead
         auto load_row = [&](const uint8_t* base, int q, uint32_t* dst) {
             const uint8_t* rr = base + (p0 + q) * E;
 #pragma unroll
             for (int r = 0; r < EWC; ++r)
                 dst[r] = (!last_partial || r < EWC - 1 || lane + 64 * r < E) ? rr[lane + 64 * r] : 0u;
         };
-        const uint8_t* pf_src = ALIAS ? slot : room;
-        if (wv < nq) load_row(pf_src, wv, pfn);
+        if (wv < nq) load_row(room, wv, pfn);
         for (int q = wv; q < nq; q += NW) {
             uint32_t rv[EWC], sv[EWC];
-            if constexpr (ALIAS) {
 #pragma unroll
-                for (int r = 0; r < EWC; ++r) sv[r] = pfn[r];
-                load_row(room, q, rv);
-            } else {
+            for (int r = 0; r < EWC; ++r) rv[r] = pfn[r];
+            const uint8_t* rs = tile + q * SP;
 #pragma unroll
-                for (int r = 0; r < EWC; ++r) rv[r] = pfn[r];
-                const uint8_t* rs = tile + q * SP;
-#pragma unroll
-                for (int r = 0; r < EWC; ++r)
-                    sv[r] = (!last_partial || r < EWC - 1 || lane + 64 * r < E) ? rs[lane + 64 * r] : 0u;
-            }
-            if (q + NW < nq) load_row(pf_src, q + NW, pfn);             // next individual
+            for (int r = 0; r < EWC; ++r)
+                sv[r] = (!last_partial || r < EWC - 1 || lane + 64 * r < E) ? rs[lane + 64 * r] : 0u;
+            if (q + NW < nq) load_row(room, q + NW, pfn);             // next individual
             // an invalid gene anywhere -> sentinel outputs; decided from registers
             uint32_t smax = 0, rmax = 0;
 #pragma unroll
@@ -710,12 +334,9 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
                         const uint32_t s = sv[r], ro = rv[r];
                         if (!(ablate & 8)) atomicOr((unsigned long long*)&B[s * EWC + r], 1ull << lane);
                         const uint32_t cell = s * (uint32_t)R + ro;
-                        if (ablate & 16) {
-                        } else if constexpr (CNT32) {
-                            h += (int)atomicAdd(&cnt[cell], 1u);                        // Solution.cpp:148-150
-                        } else {
+                        if (!(ablate & 16)) {
                             const uint32_t sh = (cell & 1u) << 4;
-                            h += (int)((atomicAdd(&cnt[cell >> 1], 1u << sh) >> sh) & 0xFFFFu);
+                            h += (int)((atomicAdd(&cnt[cell >> 1], 1u << sh) >> sh) & 0xFFFFu);   // Solution.cpp:148-150
                         }
                         const bool last_slot = (kLastSlotMask >> s) & 1ull;
                         if constexpr (PK == 1) {
@@ -765,19 +386,12 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
     }
 }
 
-// ---------------------------------------------------------------- eval_split
-// The two phases of eval_tile5 as two launches on the same stream, so that
-// each runs at the occupancy its own registers and LDS allow instead of the
-// fused kernel's common minimum (128 VGPRs for the register-resident
-// correlation words, a 26 KB tile per 64 individuals):
-//  * eval_lanes_kernel (lane = individual): stages a tile, builds the
-//    attendance masks of the wave's student range and writes the per-student
-//    scv part (>2 in a row + single class) of each individual to scv_out;
-//  * eval_waves_kernel (wave = individual, no tile, no workgroup barrier):
-//    slot and room rows straight from global memory (one individual ahead),
-//    the hcv terms and the last-slot term; it adds the latter to scv_out and
-//    writes the final four outputs.
-template <int NWL>
+// ---------------------------------------------------------------- eval_lanes
+// The lane phase of eval_tile5 on its own (wide path, E > 448): a 16-wave
+// workgroup per 64-row tile (128 KB at E = 2000: one workgroup per CU); it
+// writes the per-student scv part (>2 in a row + single class) of each
+// individual to scv_part, which eval_corr completes.
+template <int NWL, int U>
 __global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, const uint8_t* __restrict__ slot, int P,
                                                               int32_t* __restrict__ scv_part) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -820,29 +434,7 @@ __global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, con
         }
         if (threadIdx.x < 64) tile[threadIdx.x * SP + E] = 63;
         __syncthreads();
-        int sc = 0;
-        if (c0 < c1) {
-            const uint8_t* my = tile + lane * SP;
-            uint32_t cur[4] = {rec[4 * c0], rec[4 * c0 + 1], rec[4 * c0 + 2], rec[4 * c0 + 3]};
-            uint64_t m = 0;
-            for (int c = c0; c < c1; ++c) {
-                const int cn = c + 1 < c1 ? c + 1 : c;
-                const uint32_t nxt[4] = {rec[4 * cn], rec[4 * cn + 1], rec[4 * cn + 2], rec[4 * cn + 3]};
-                uint32_t sl[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) sl[j] = my[(cur[j >> 1] >> (16 * (j & 1))) & 0x7FFFu];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) m |= 1ull << (sl[j] & 63);
-                if (cur[0] & 0x8000u) {                                  // last record of a student
-                    sc += __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);   // Solution.cpp:99-117
-#pragma unroll
-                    for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);   // :119-137
-                    m = 0;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
-            }
-        }
+        const int sc = c0 < c1 ? lane_scv<U>(tile + lane * SP, rec, c0, c1) : 0;
         part[wv * 64 + lane] = sc;
         __syncthreads();
         if (wv == 0 && lane < np) {
@@ -854,269 +446,262 @@ __global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, con
     }
 }
 
-constexpr int kWavesWG = 4;   // waves per workgroup of eval_waves_kernel
-constexpr int kWideWG = 8;    // waves per workgroup of eval_wide_kernel (one individual each)
-constexpr int kWideMaxNC = 10; // eval_wide handles E <= 256 * kWideMaxNC
-
-template <int EWC, int PK>
-__global__ __launch_bounds__(64 * kWavesWG, 4) void eval_waves_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
-                                                                      const uint8_t* __restrict__ room, int P,
-                                                                      int32_t* __restrict__ hcv_out,
-                                                                      int32_t* __restrict__ scv_io,
-                                                                      uint8_t* __restrict__ feas_out,
-                                                                      int32_t* __restrict__ pen_out, int WS) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int E = pb.E, R = pb.R;
-    const int lane = threadIdx.x & 63, wv = wave_id();
-    uint8_t* ws = lds + (size_t)wv * WS;
-    uint64_t* B = (uint64_t*)ws;                              // [45][EWC] event bitsets per slot
-    uint32_t* cnt = (uint32_t*)(B + kSlots * EWC);            // packed u16 cell counters
-    const bool last_partial = E < 64 * EWC;
-
-    using PossT = typename std::conditional<PK == 0, uint64_t, uint32_t>::type;
-    uint64_t inv_cup[EWC][EWC];
-    PossT inv_poss[EWC];
-    uint32_t inv_ps[EWC];
-    int inv_sn[EWC];
-#pragma unroll
-    for (int r = 0; r < EWC; ++r) {
-        const int e = lane + 64 * r;
-        const bool ok = e < E;
-        if constexpr (PK == 1) {
-            inv_ps[r] = ok ? ((uint32_t)pb.poss[e] | ((uint32_t)pb.sn[e] << 16)) : 0xFFFFu;
-        } else {
-            inv_poss[r] = ok ? (PossT)pb.poss[e] : (PossT)~0ull;
-            inv_sn[r] = ok ? pb.sn[e] : 0;
-        }
-#pragma unroll
-        for (int w = 0; w < EWC; ++w) inv_cup[r][w] = (w >= r && ok) ? pb.cupT[(size_t)w * E + e] : 0ull;
-    }
-    auto load_row = [&](const uint8_t* base, long q, uint32_t* dst) {
-        const uint8_t* rr = base + q * E;
-#pragma unroll
-        for (int r = 0; r < EWC; ++r)
-            dst[r] = (!last_partial || r < EWC - 1 || lane + 64 * r < E) ? rr[lane + 64 * r] : 0u;
-    };
-    const long GW = (long)gridDim.x * kWavesWG;
-    long q = (long)blockIdx.x * kWavesWG + wv;
-    uint32_t svn[EWC], rvn[EWC];
-    if (q < P) { load_row(slot, q, svn); load_row(room, q, rvn); }
-    for (; q < P; q += GW) {
-        uint32_t sv[EWC], rv[EWC];
-#pragma unroll
-        for (int r = 0; r < EWC; ++r) { sv[r] = svn[r]; rv[r] = rvn[r]; }
-        if (q + GW < P) { load_row(slot, q + GW, svn); load_row(room, q + GW, rvn); }
-        uint32_t smax = 0, rmax = 0;
-#pragma unroll
-        for (int r = 0; r < EWC; ++r) { smax = max(smax, sv[r]); rmax = max(rmax, rv[r]); }
-        const bool any_bad = __any(smax >= (uint32_t)kSlots || rmax >= (uint32_t)R);
-        int h = 0, last = 0;
-        if (!any_bad) {
-            for (int c = lane; c < (WS >> 4); c += 64) ((uint4*)ws)[c] = make_uint4(0u, 0u, 0u, 0u);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int r = 0; r < EWC; ++r) {
-                if (r < EWC - 1 || !last_partial || lane + 64 * r < E) {
-                    const uint32_t s = sv[r], ro = rv[r];
-                    atomicOr((unsigned long long*)&B[s * EWC + r], 1ull << lane);
-                    const uint32_t cell = s * (uint32_t)R + ro, sh = (cell & 1u) << 4;
-                    h += (int)((atomicAdd(&cnt[cell >> 1], 1u << sh) >> sh) & 0xFFFFu);   // Solution.cpp:148-150
-                    const bool last_slot = (kLastSlotMask >> s) & 1ull;
-                    if constexpr (PK == 1) {
-                        h += (int)(((inv_ps[r] >> ro) & 1u) ^ 1u);                  // :155-156
-                        last += last_slot ? (int)(inv_ps[r] >> 16) : 0;             // :93-96
-                    } else {
-                        h += (int)(((inv_poss[r] >> ro) & 1u) ^ 1u);
-                        last += last_slot ? inv_sn[r] : 0;
-                    }
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            corr_words<0, EWC>(lds_addr(B), sv, inv_cup, lane, E, last_partial, h);   // :151-153
-            h = wave_sum(h);
-            last = wave_sum(last);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        if (lane == 0) {
-            if (any_bad) {
-                hcv_out[q] = -1; scv_io[q] = -1; feas_out[q] = 0; pen_out[q] = -1;
-            } else {
-                const int s2 = scv_io[q] + last;
-                hcv_out[q] = h;
-                scv_io[q] = s2;
-                feas_out[q] = h == 0 ? 1 : 0;
-                pen_out[q] = h == 0 ? s2 : 1000000 + h;
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------- eval_wide
-// The wave phase for instances too wide for eval_tile5's register-resident
-// correlation words (E > 448, e.g. the 2000-event synthetic instance), run
-// after eval_lanes_kernel<16> (which writes the per-student scv part):
-// wave = individual, NW waves (NW individuals) per workgroup, lane l owns
-// events e = 256 c + 4 l + k (k < 4) of every 256-event chunk c < NC, so its
-// slot/room bytes arrive as one dword per chunk and its invariants
-// (possibleRooms, studentNumber, upper-triangle words) as 16-B vector loads.
-// The upper-triangle words (E x EW64 / 2 u64, 256 KB at E = 2000) are the
-// dominant stream: the waves of a workgroup walk them in the same order and
-// meet at a barrier per chunk, so one wave's L2 fetch is the others' L1 hit.
-// Per-wave LDS workspace: event bitsets B[45][BST] (BST = EW64 | 1 u64 words:
-// an odd row stride spreads the 45 rows over the banks) and packed u16
-// room-cell counters.
-//   hcv  = sum over cells of C(n, 2)                (Solution.cpp:148-150, ds_add_rtn)
+// ---------------------------------------------------------------- eval_corr
+// The hcv terms (and the last-slot scv term) of the wide path, after
+// eval_lanes. The upper-triangle correlation stream (E x EW64 / 2 u64 words,
+// 264 KB at E = 2000) is the same for every individual, so a workgroup reads
+// it once per batch of NB individuals instead of once per individual:
+//  * build phase: wave v owns EPL consecutive events per lane (their
+//    possibleRooms / studentNumber stay in registers) and, for every
+//    individual of the batch, sets the slot bitsets B_q[45][BST] (ds_or_b64),
+//    counts room cells in packed u16 counters (ds_add_rtn: the returned old
+//    counts sum to sum_cells C(n,2)), adds unsuitable rooms and the last-slot
+//    term and stages the slot row in LDS;
+//  * corr phase: the 64-event chunks are taken in pairs (a, EW64-1-a), so
+//    every pair has EW64+1 upper-triangle words per event; wave v streams the
+//    words w >= c of its chunks' events (coalesced 512-B loads, four words
+//    ahead) and, for each word, gathers B_q[slot][w] of all NB individuals
+//    (NB independent ds_read_b64 in flight) and adds popcount(word & B word).
+// Per-individual LDS: B rows (odd u64 stride BST = EW64 | 1), counters, slot row.
+//   hcv  = sum over cells of C(n, 2)                (Solution.cpp:148-150)
 //        + sum_e [room_e not possible]              (:155-156)
 //        + sum_e sum_{w >= e/64} popcount(cupT[w][e] & B[slot_e][w])   (:151-153)
 //   scv += sum_e [slot_e % 9 == 8] studentNumber[e] (:93-96)
-template <int NC, int NW>
-__global__ __launch_bounds__(64 * NW) void eval_wide_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
-                                                            const uint8_t* __restrict__ room, int P,
-                                                            int32_t* __restrict__ hcv_out,
-                                                            int32_t* __restrict__ scv_io,
-                                                            uint8_t* __restrict__ feas_out,
-                                                            int32_t* __restrict__ pen_out, int BST, int WS,
-                                                            int ablate) {
+struct CorrLayout {
+    int NWV, BST, NB, EPL;
+    size_t off_cnt, off_sl, WSI, off_acc, bytes;
+};
+
+__host__ __device__ inline CorrLayout corr_layout(int E, int R, int EW64, int NB) {
+    CorrLayout L;
+    const int pairs = (EW64 + 1) / 2;
+    L.NWV = pairs < 16 ? pairs : 16;
+    L.EPL = (E + 64 * L.NWV - 1) / (64 * L.NWV);
+    L.BST = EW64 | 1;
+    L.off_cnt = (size_t)kSlots * L.BST * 8;
+    L.off_sl = L.off_cnt + (size_t)((kSlots * R + 1) / 2) * 4;
+    L.WSI = (L.off_sl + (size_t)E + 15) & ~(size_t)15;
+    L.NB = NB;
+    L.off_acc = (size_t)NB * L.WSI;
+    L.bytes = L.off_acc + (size_t)NB * 16;
+    return L;
+}
+
+constexpr int kCorrMaxEPL = 4;
+
+// N ds_read_b64 at N per-lane byte addresses + OFF, all in flight at once,
+// waited for inside the asm (results defined when it ends).
+template <int N, int OFF>
+__device__ __forceinline__ void lds_gather(const uint32_t* a, uint64_t* v) {
+    static_assert(N == 2 || N == 4 || N == 8, "2, 4 or 8 reads");
+    if constexpr (N == 8)
+        asm volatile("ds_read_b64 %0, %8 offset:%16\n ds_read_b64 %1, %9 offset:%16\n ds_read_b64 %2, %10 offset:%16\n"
+                     "ds_read_b64 %3, %11 offset:%16\n ds_read_b64 %4, %12 offset:%16\n ds_read_b64 %5, %13 offset:%16\n"
+                     "ds_read_b64 %6, %14 offset:%16\n ds_read_b64 %7, %15 offset:%16\n s_waitcnt lgkmcnt(0)"
+                     : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+                     : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "i"(OFF)
+                     : "memory");
+    else if constexpr (N == 4)
+        asm volatile("ds_read_b64 %0, %4 offset:%8\n ds_read_b64 %1, %5 offset:%8\n ds_read_b64 %2, %6 offset:%8\n"
+                     "ds_read_b64 %3, %7 offset:%8\n s_waitcnt lgkmcnt(0)"
+                     : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+                     : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "i"(OFF) : "memory");
+    else
+        asm volatile("ds_read_b64 %0, %2 offset:%4\n ds_read_b64 %1, %3 offset:%4\n s_waitcnt lgkmcnt(0)"
+                     : "=&v"(v[0]), "=&v"(v[1]) : "v"(a[0]), "v"(a[1]), "i"(OFF) : "memory");
+}
+
+// Words c..EW-1 of event 64c+lane (upper-triangle correlation words, cupT
+// word-major) against NB individuals whose B rows for this event's slot start
+// at LDS byte addresses r[q]: h[q] += popcount(word & B_q word). Blocks of 4
+// words: the next block's global loads are issued before this block's gathers.
+template <int NB>
+__device__ __forceinline__ void corr_chunk(const DevProblem& pb, int c, int lane, const uint32_t (&r)[NB], int (&h)[NB]) {
+    const int E = pb.E, EW = pb.EW64, e = 64 * c + lane;
+    const bool ev = e < E;
+    const uint64_t* src = pb.cupT + (ev ? e : 0);
+    uint64_t x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = (ev && c + j < EW) ? src[(size_t)(c + j) * E] : 0ull;
+    for (int w = c; w < EW; w += 4) {
+        uint64_t y[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[j] = (ev && w + 4 + j < EW) ? src[(size_t)(w + 4 + j) * E] : 0ull;
+        uint32_t b[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) b[q] = r[q] + 8u * (uint32_t)w;
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            ([&] {
+                if (w + J < EW) {                                  // wave-uniform
+                    uint64_t v[NB];
+                    lds_gather<NB, 8 * J>(b, v);
+#pragma unroll
+                    for (int q = 0; q < NB; ++q) h[q] = popc_acc(x[J] & v[q], h[q]);
+                }
+            }(), ...);
+        }(std::make_integer_sequence<int, 4>{});
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[j] = y[j];
+    }
+}
+
+template <int NB>
+__global__ __launch_bounds__(1024) void eval_corr_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
+                                                         const uint8_t* __restrict__ room, int P,
+                                                         int32_t* __restrict__ hcv_out, int32_t* __restrict__ scv_io,
+                                                         uint8_t* __restrict__ feas_out, int32_t* __restrict__ pen_out,
+                                                         int ablate) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int E = pb.E, R = pb.R, EW64 = pb.EW64;
+    const int E = pb.E, R = pb.R, EW = pb.EW64;
+    const CorrLayout L = corr_layout(E, R, EW, NB);
     const int lane = threadIdx.x & 63, wv = wave_id();
-    uint8_t* ws = lds + (size_t)wv * WS;
-    uint64_t* B = (uint64_t*)ws;                              // [45][BST]
-    uint32_t* cnt = (uint32_t*)(B + kSlots * BST);            // packed u16 cell counters
-    // dword row loads and 16-B upper-triangle loads need E % 4 == 0 and aligned rows
-    const bool al = (E & 3) == 0 && (((uintptr_t)slot | (uintptr_t)room) & 3) == 0;
-    const int groups = (P + NW - 1) / NW;
-    for (int g = blockIdx.x; g < groups; g += gridDim.x) {     // every wave runs every barrier
-        const long q = (long)g * NW + wv;
-        const bool act = q < P;
-        uint32_t sv[NC], rv[NC];                              // bytes k = events 256c + 4 lane + k
-        int nv[NC];                                           // valid events of the lane in chunk c
-        bool bad = false;
-        const uint8_t* srow = slot + (act ? q : 0) * E;
-        const uint8_t* rrow = room + (act ? q : 0) * E;
+    const int NWV = L.NWV, pairs = (EW + 1) / 2, EPL = L.EPL;
+    const uint32_t WSI = (uint32_t)L.WSI, BSTB = (uint32_t)L.BST * 8u;
+    int32_t* acc = (int32_t*)(lds + L.off_acc);                  // [NB][4]: h, last, bad, -
+    const uint32_t lds0 = lds_addr(lds);
+
+    // build-phase events of this lane and their invariants
+    const int eb = (wv * 64 + lane) * EPL;
+    // two events per lane from 2-byte aligned rows: one u16 load each
+    const bool pair16 = EPL == 2 && (E & 1) == 0 && (((uintptr_t)slot | (uintptr_t)room) & 1) == 0;
+    uint64_t possv[kCorrMaxEPL];
+    int snv[kCorrMaxEPL];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            const int e0 = 256 * c + 4 * lane;
-            nv[c] = act ? max(0, min(4, E - e0)) : 0;
-            if (al && nv[c] == 4) {
-                sv[c] = *(const uint32_t*)(srow + e0);
-                rv[c] = *(const uint32_t*)(rrow + e0);
-            } else {
-                sv[c] = 0u; rv[c] = 0u;
-                for (int k = 0; k < nv[c]; ++k) {
-                    sv[c] |= (uint32_t)srow[e0 + k] << (8 * k);
-                    rv[c] |= (uint32_t)rrow[e0 + k] << (8 * k);
-                }
-            }
+    for (int j = 0; j < kCorrMaxEPL; ++j) {
+        const bool ok = j < EPL && eb + j < E;
+        possv[j] = ok ? pb.poss[eb + j] : ~0ull;
+        snv[j] = ok ? pb.sn[eb + j] : 0;
+    }
+
+    const long batches = ((long)P + NB - 1) / NB;
+    for (long bt = blockIdx.x; bt < batches; bt += gridDim.x) {
+        const long q0 = bt * NB;
+        const int nq = (int)min((long)NB, (long)P - q0);
+        __syncthreads();                                         // previous batch's outputs are read
+        for (int i = threadIdx.x; i < (int)(L.off_acc >> 4) + NB; i += blockDim.x)
+            ((uint4*)lds)[i] = make_uint4(0u, 0u, 0u, 0u);       // workspaces + acc
+        __syncthreads();
+        // ---- build phase: the lane's events for every individual of the batch
+        if (!(ablate & 1)) {
+            // every individual's bytes in flight at once (the rows come from HBM)
+            uint32_t svq[NB], rvq[NB];
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k < nv[c]) bad |= ((sv[c] >> (8 * k)) & 0xFFu) >= (uint32_t)kSlots || ((rv[c] >> (8 * k)) & 0xFFu) >= (uint32_t)R;
-        }
-        const bool work = act && !__any(bad);                 // wave-uniform
-        int h = 0, last = 0;
-        if (work && !(ablate & 1)) {
-            for (int i = lane; i < (WS >> 4); i += 64) ((uint4*)ws)[i] = make_uint4(0u, 0u, 0u, 0u);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int q = 0; q < NB; ++q) {
+                svq[q] = 0u; rvq[q] = 0u;
+                if (q < nq) {
+                    const uint8_t* srow = slot + (q0 + q) * E + eb;
+                    const uint8_t* rrow = room + (q0 + q) * E + eb;
+                    if (pair16 && eb + 1 < E) {
+                        svq[q] = *(const uint16_t*)srow;
+                        rvq[q] = *(const uint16_t*)rrow;
+                    } else {
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                const int e0 = 256 * c + 4 * lane;
-                if (nv[c] == 0) continue;
-                uint64_t poss[4];
-                int sn[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    poss[k] = k < nv[c] ? pb.poss[e0 + k] : ~0ull;
-                    sn[k] = k < nv[c] ? pb.sn[e0 + k] : 0;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (k < nv[c]) {
-                        const int e = e0 + k;
-                        const uint32_t s = (sv[c] >> (8 * k)) & 0xFFu, ro = (rv[c] >> (8 * k)) & 0xFFu;
-                        atomicOr((unsigned long long*)&B[s * (uint32_t)BST + (uint32_t)(e >> 6)], 1ull << (e & 63));
-                        const uint32_t cell = s * (uint32_t)R + ro, sh = (cell & 1u) << 4;
-                        h += (int)((atomicAdd(&cnt[cell >> 1], 1u << sh) >> sh) & 0xFFFFu);
-                        h += (int)(((poss[k] >> ro) & 1ull) ^ 1ull);
-                        last += ((kLastSlotMask >> s) & 1ull) ? sn[k] : 0;
+                        for (int j = 0; j < kCorrMaxEPL; ++j)
+                            if (j < EPL && eb + j < E) {
+                                svq[q] |= (uint32_t)srow[j] << (8 * j);
+                                rvq[q] |= (uint32_t)rrow[j] << (8 * j);
+                            }
                     }
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        // correlated same-slot pairs: the words w >= 4c hold every upper-triangle
-        // bit of chunk c's events (bits j > e live in words >= e/64 >= 4c)
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            __syncthreads();                                  // keep the group's waves on the same words
-            const int e0 = 256 * c + 4 * lane;
-            if (work && nv[c] > 0 && !(ablate & 2)) {
-                uint32_t boff[4];
+            for (int q = 0; q < NB; ++q) {
+                if (q >= nq) break;                              // wave-uniform
+                const uint32_t sv = svq[q], rv = rvq[q];
+                uint8_t* wsq = lds + (size_t)q * WSI;
+                uint64_t* B = (uint64_t*)wsq;
+                uint32_t* cnt = (uint32_t*)(wsq + L.off_cnt);
+                int h = 0, last = 0;
+                bool bad = false;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) boff[k] = ((sv[c] >> (8 * k)) & 0xFFu) * (uint32_t)BST;
-                if (al) {                                     // nv[c] == 4; 32-B aligned words
-#pragma unroll 4
-                    for (int w = 4 * c; w < EW64; ++w) {
-                        const uint4* cw = (const uint4*)(pb.cupT + (size_t)w * E + e0);
-                        const uint4 x = cw[0], y = cw[1];
-                        h += __popcll((((uint64_t)x.y << 32) | x.x) & B[boff[0] + (uint32_t)w]);
-                        h += __popcll((((uint64_t)x.w << 32) | x.z) & B[boff[1] + (uint32_t)w]);
-                        h += __popcll((((uint64_t)y.y << 32) | y.x) & B[boff[2] + (uint32_t)w]);
-                        h += __popcll((((uint64_t)y.w << 32) | y.z) & B[boff[3] + (uint32_t)w]);
+                for (int j = 0; j < kCorrMaxEPL; ++j) {
+                    const int e = eb + j;
+                    if (j < EPL && e < E) {
+                        const uint32_t s = (sv >> (8 * j)) & 0xFFu, ro = (rv >> (8 * j)) & 0xFFu;
+                        wsq[L.off_sl + e] = (uint8_t)min(s, (uint32_t)kSlots - 1);   // slot row for the corr phase
+                        if (s >= (uint32_t)kSlots || ro >= (uint32_t)R) {
+                            bad = true;
+                        } else {
+                            atomicOr((unsigned long long*)&B[s * (uint32_t)L.BST + (uint32_t)(e >> 6)], 1ull << (e & 63));
+                            const uint32_t cell = s * (uint32_t)R + ro, sh = (cell & 1u) << 4;
+                            h += (int)((atomicAdd(&cnt[cell >> 1], 1u << sh) >> sh) & 0xFFFFu);
+                            h += (int)(((possv[j] >> ro) & 1ull) ^ 1ull);
+                            last += ((kLastSlotMask >> s) & 1ull) ? snv[j] : 0;
+                        }
                     }
-                } else {
-#pragma unroll 2
-                    for (int w = 4 * c; w < EW64; ++w) {
-                        const uint64_t* cw = pb.cupT + (size_t)w * E + e0;
-#pragma unroll
-                        for (int k = 0; k < 4; ++k)
-                            if (k < nv[c]) h += __popcll(cw[k] & B[boff[k] + (uint32_t)w]);
-                    }
+                }
+                h = wave_sum(h);
+                last = wave_sum(last);
+                const bool anyb = __any(bad);
+                if (lane == 0) {
+                    atomicAdd(&acc[4 * q], h);
+                    atomicAdd(&acc[4 * q + 1], last);
+                    if (anyb) atomicOr(&acc[4 * q + 2], 1);
                 }
             }
         }
-        if (work) {
-            h = wave_sum(h);
-            last = wave_sum(last);
+        __syncthreads();
+        // ---- corr phase: the wave's chunk pair against every individual of the batch
+        if (!(ablate & 2)) {
+            for (int pr = wv; pr < pairs; pr += NWV) {             // wave-uniform
+                const int ca = pr, cb = EW - 1 - pr;
+                int hq[NB];
+#pragma unroll
+                for (int q = 0; q < NB; ++q) hq[q] = 0;
+#pragma unroll
+                for (int side = 0; side < 2; ++side) {
+                    const int c = side ? cb : ca;
+                    if (side && cb == ca) break;
+                    const int e = 64 * c + lane;
+                    // per individual: LDS byte address of word 0 of the B row of e's slot
+                    uint32_t r[NB];
+#pragma unroll
+                    for (int q = 0; q < NB; ++q) {
+                        const uint32_t sq = (q < nq && e < E) ? (uint32_t)lds[(size_t)q * WSI + L.off_sl + e] : 0u;
+                        r[q] = lds0 + (q < nq ? q : 0) * WSI + sq * BSTB;
+                    }
+                    corr_chunk<NB>(pb, c, lane, r, hq);
+                }
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    if (q >= nq) break;
+                    const int h = wave_sum(hq[q]);
+                    if (lane == 0) atomicAdd(&acc[4 * q], h);
+                }
+            }
         }
-        if (act && lane == 0) {
-            if (!work) {
+        __syncthreads();
+        if (threadIdx.x < nq) {
+            const long q = q0 + threadIdx.x;
+            const int* a = acc + 4 * threadIdx.x;
+            if (a[2]) {
                 hcv_out[q] = -1; scv_io[q] = -1; feas_out[q] = 0; pen_out[q] = -1;
             } else {
-                const int s2 = scv_io[q] + last;
+                const int h = a[0], s2 = scv_io[q] + a[1];
                 hcv_out[q] = h;
                 scv_io[q] = s2;
                 feas_out[q] = h == 0 ? 1 : 0;
                 pen_out[q] = h == 0 ? s2 : 1000000 + h;
             }
         }
-        __syncthreads();                                      // workspaces are reused by the next group
     }
 }
 
-struct WideLayout {
-    int BST, WS;
-    size_t lanes_bytes;
-};
-
-// LDS of the wide path: eval_lanes_kernel<16> tile + partials, per-wave workspace of eval_wide_kernel.
-static WideLayout wide_layout(int E, int R, int EW64) {
-    WideLayout L;
-    L.BST = EW64 | 1;
-    L.WS = (kSlots * L.BST * 8 + ((kSlots * R + 1) / 2) * 4 + 15) & ~15;
+// LDS of eval_lanes<16>: the 64-row tile + partials.
+static size_t lanes_lds_bytes(int E) {
     int sp = (E + 1 + 3) & ~3;
     if (((sp >> 2) & 1) == 0) sp += 4;
-    L.lanes_bytes = (((size_t)64 * sp + 15) & ~(size_t)15) + 4 * (size_t)16 * 64;
-    return L;
+    return (((size_t)64 * sp + 15) & ~(size_t)15) + 4 * (size_t)16 * 64;
+}
+
+constexpr size_t kCorrLdsBudget = 152 * 1024;
+
+// Batch size of eval_corr: the largest of 8, 4, 2 whose workspaces fit the LDS
+// (0: none).
+static int corr_nb(int E, int R, int EW64) {
+    for (int nb = 8; nb >= 2; nb >>= 1)
+        if (corr_layout(E, R, EW64, nb).bytes <= kCorrLdsBudget) return nb;
+    return 0;
 }
 
 // ---------------------------------------------------------------- eval_block
@@ -1218,15 +803,22 @@ static size_t block_lds_bytes(int E, int R) {
 
 using namespace ttga;
 
+static bool tile5_fits(const tt_problem* p, int NW) {
+    return p->dev.EW64 <= 7 && p->E <= 32767 && tile5_layout(p->E, p->R, NW).bytes <= (NW == 8 ? 80 : 160) * 1024;
+}
+
+static bool wide_fits(const tt_problem* p) {
+    const int EW64 = p->dev.EW64;
+    return p->E <= 32767 && lanes_lds_bytes(p->E) <= 160 * 1024 &&
+           corr_nb(p->E, p->R, EW64) > 0 && corr_layout(p->E, p->R, EW64, 2).EPL <= kCorrMaxEPL;
+}
+
 // The kernel tt_eval runs for this instance (see tt_eval_variant).
 static int auto_variant(const tt_problem* p) {
-    const int E = p->E, R = p->R;
-    if (p->dev.EW64 <= 7 && E <= 32767 && tile5_layout(E, R, 8, false, false).bytes <= 80 * 1024) return 8;
-    if (p->dev.EW64 <= 7 && tile4_layout(E, R, 4).bytes <= 64 * 1024) return 3;
-    const WideLayout WL = wide_layout(E, R, p->dev.EW64);
-    if (E <= 256 * kWideMaxNC && E <= 32767 && WL.lanes_bytes <= 160 * 1024 && (size_t)(kWideWG / 2) * WL.WS <= 160 * 1024)
-        return 13;
-    return (E <= 1024 && tile_layout(E, R).bytes <= 80 * 1024) ? 1 : 2;
+    if (tile5_fits(p, 8)) return 8;
+    if (tile5_fits(p, 4)) return 7;
+    if (wide_fits(p)) return 13;
+    return 2;
 }
 
 extern "C" int tt_eval_auto_variant(const tt_problem* p) { return p ? auto_variant(p) : -1; }
@@ -1236,149 +828,56 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
     int rc = check_pop_args(p, P, slot, room);
     if (rc) return rc;
     if (P > 0 && (!hcv || !scv || !feasible || !penalty)) { set_error("null output buffer"); return TT_ERR_INVALID; }
-    // profiling-only phase switches (results invalid): 1 lane phase, 2 wave phase, 4 correlation
-    // words, 8 B-bitset atomics, 16 cell-counter atomics, 32 workspace zeroing (eval_tile5);
-    // 1 atomics + zeroing, 2 correlation words (eval_wide)
+    // profiling-only phase switches (results invalid): eval_tile5: 1 lane phase, 2 wave
+    // phase, 4 correlation words, 8 B-bitset atomics, 16 cell-counter atomics, 32
+    // workspace zeroing; wide path: 1 eval_corr build phase, 2 eval_corr corr phase,
+    // 4 no eval_corr launch, 8 eval_lanes without the record prefetch (valid results)
     const int ablate = variant >> 4;
     variant &= 15;
-    if (variant < 0 || variant > 13) { set_error("unknown eval variant"); return TT_ERR_INVALID; }
+    if (variant != 0 && variant != 2 && variant != 7 && variant != 8 && variant != 13) {
+        set_error("unknown eval variant (0 auto, 2 block, 7/8 tile5, 13 wide)");
+        return TT_ERR_INVALID;
+    }
     if (P == 0) return TT_OK;
     rc = use_device(p);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     const int E = p->E, R = p->R;
-    const TileLayout TL = tile_layout(E, R);
     if (variant == 0) variant = auto_variant(p);
-    if (variant == 1) {
-        if (TL.bytes > 160 * 1024) { set_error("instance too large for the tile kernel"); return TT_ERR_LIMIT; }
+    if (variant == 13) {
+        // wide path: eval_lanes<16> (tile of 64 rows, lane phase) then eval_corr
+        if (!wide_fits(p)) { set_error("instance outside the wide eval path"); return TT_ERR_LIMIT; }
+        const int EW64 = p->dev.EW64;
         const int tiles = (P + 63) / 64;
-        const dim3 b(64 * kTileWaves);
-        auto launch = [&](auto kern) -> int {
-            int per_cu = 0;
-            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, b.x, TL.bytes));
-            const int grid = std::min(tiles, std::max(1, per_cu) * p->num_cus);
-            hipLaunchKernelGGL(kern, dim3(grid), b, TL.bytes, st, p->dev, slot, room, P, hcv, scv, feasible, penalty,
-                               ablate);
-            return TT_OK;
-        };
-        switch (p->dev.EW64) {
-            case 1: rc = launch(eval_tile_kernel<1>); break;
-            case 2: rc = launch(eval_tile_kernel<2>); break;
-            case 3: rc = launch(eval_tile_kernel<3>); break;
-            case 4: rc = launch(eval_tile_kernel<4>); break;
-            case 5: rc = launch(eval_tile_kernel<5>); break;
-            case 6: rc = launch(eval_tile_kernel<6>); break;
-            case 7: rc = launch(eval_tile_kernel<7>); break;
-            default: rc = launch(eval_tile_kernel<0>); break;
+        {
+            const size_t lds_l = lanes_lds_bytes(E);
+            auto launch_l = [&](auto kern) -> int {
+                int per_cu = 0;
+                TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 1024, lds_l));
+                const int grid = std::min(tiles, std::max(1, per_cu) * p->num_cus);
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), lds_l, st, p->dev, slot, P, scv);
+                return TT_OK;
+            };
+            rc = (ablate & 8) ? launch_l(eval_lanes_kernel<16, 1>) : launch_l(eval_lanes_kernel<16, kLanePF>);
+            if (rc) return rc;
         }
-        if (rc) return rc;
-    } else if (variant == 3 || variant == 4) {
-        const int NW = variant == 3 ? 4 : 8;
-        const Tile4Layout TL4 = tile4_layout(E, R, NW);
-        if (p->dev.EW64 > 7 || TL4.bytes > 160 * 1024) { set_error("instance too large for the tile4 kernel"); return TT_ERR_LIMIT; }
-        const int max_sn = p->student_number.empty() ? 0 : *std::max_element(p->student_number.begin(), p->student_number.end());
-        const int pk = (R <= 16 && max_sn <= 0xFFFF) ? 1 : R <= 32 ? 2 : 0;
-        const int tiles = (P + 63) / 64;
+        if (ablate & 4) return check_hip(hipGetLastError(), "tt_eval launch");   // lane phase only (timing)
+        const int NB = corr_nb(E, R, EW64);
+        const CorrLayout CL = corr_layout(E, R, EW64, NB);
         auto launch = [&](auto kern) -> int {
             int per_cu = 0;
-            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, TL4.bytes));
-            const int grid = std::min(tiles, std::max(1, per_cu) * p->num_cus);
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NW), TL4.bytes, st, p->dev, slot, room, P, hcv, scv,
+            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * CL.NWV, CL.bytes));
+            const long batches = ((long)P + NB - 1) / NB;
+            const int grid = (int)std::min<long>(batches, (long)std::max(1, per_cu) * p->num_cus);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * CL.NWV), CL.bytes, st, p->dev, slot, room, P, hcv, scv,
                                feasible, penalty, ablate);
             return TT_OK;
         };
-#define TT_T4(EWC)                                                                              \
-    case EWC:                                                                                   \
-        if (NW == 4) rc = pk == 1 ? launch(eval_tile4_kernel<EWC, 4, 1>) : pk == 2 ? launch(eval_tile4_kernel<EWC, 4, 2>) \
-                                  : launch(eval_tile4_kernel<EWC, 4, 0>);                                         \
-        else rc = pk == 1 ? launch(eval_tile4_kernel<EWC, 8, 1>) : pk == 2 ? launch(eval_tile4_kernel<EWC, 8, 2>)     \
-                          : launch(eval_tile4_kernel<EWC, 8, 0>);                                                 \
-        break;
-        switch (p->dev.EW64) {
-            TT_T4(1) TT_T4(2) TT_T4(3) TT_T4(4) TT_T4(5) TT_T4(6) TT_T4(7)
-            default: rc = TT_ERR_LIMIT; break;
-        }
-#undef TT_T4
+rc = NB == 8 ? launch(eval_corr_kernel<8>) : NB == 4 ? launch(eval_corr_kernel<4>) : launch(eval_corr_kernel<2>);
         if (rc) return rc;
-    } else if (variant == 9 || variant == 10) {
-        // eval_lanes (8 or 4 waves per tile) then eval_waves, both on `st`
-        if (p->dev.EW64 > 7 || E > 32767) { set_error("instance too large for the split kernels"); return TT_ERR_LIMIT; }
-        const int NWL = variant == 9 ? 8 : 4;
-        int sp = (E + 1 + 3) & ~3;
-        if (((sp >> 2) & 1) == 0) sp += 4;
-        const size_t lds_l = (((size_t)64 * sp + 15) & ~(size_t)15) + 4 * (size_t)NWL * 64;
-        const int tiles = (P + 63) / 64;
-        auto launch_l = [&](auto kern) -> int {
-            int per_cu = 0;
-            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NWL, lds_l));
-            const int grid = std::min(tiles, std::max(1, per_cu) * p->num_cus);
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NWL), lds_l, st, p->dev, slot, P, scv);
-            return TT_OK;
-        };
-        rc = NWL == 8 ? launch_l(eval_lanes_kernel<8>) : launch_l(eval_lanes_kernel<4>);
-        if (rc) return rc;
-        const int WS = tile5_layout(E, R, 8, false, false).WS;
-        const size_t lds_w = (size_t)kWavesWG * WS;
-        const int max_sn = p->student_number.empty() ? 0 : *std::max_element(p->student_number.begin(), p->student_number.end());
-        const int pk = (R <= 16 && max_sn <= 0xFFFF) ? 1 : R <= 32 ? 2 : 0;
-        auto launch_w = [&](auto kern) -> int {
-            int per_cu = 0;
-            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kWavesWG, lds_w));
-            const int grid = std::min((P + kWavesWG - 1) / kWavesWG, std::max(1, per_cu) * p->num_cus);
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kWavesWG), lds_w, st, p->dev, slot, room, P, hcv, scv,
-                               feasible, penalty, WS);
-            return TT_OK;
-        };
-#define TT_TW(EWC)                                                                                  \
-    case EWC:                                                                                       \
-        rc = pk == 1 ? launch_w(eval_waves_kernel<EWC, 1>) : pk == 2 ? launch_w(eval_waves_kernel<EWC, 2>) \
-                     : launch_w(eval_waves_kernel<EWC, 0>);                                          \
-        break;
-        switch (p->dev.EW64) {
-            TT_TW(1) TT_TW(2) TT_TW(3) TT_TW(4) TT_TW(5) TT_TW(6) TT_TW(7)
-            default: rc = TT_ERR_LIMIT; break;
-        }
-#undef TT_TW
-        if (rc) return rc;
-    } else if (variant == 13) {
-        // wide path: eval_lanes<16> (tile of 64 rows, lane phase) then eval_wide (wave = individual)
-        const WideLayout WL = wide_layout(E, R, p->dev.EW64);
-        if (E > 256 * kWideMaxNC || E > 32767 || WL.lanes_bytes > 160 * 1024 || (size_t)(kWideWG / 2) * WL.WS > 160 * 1024) {
-            set_error("instance outside the wide eval path");
-            return TT_ERR_LIMIT;
-        }
-        const int tiles = (P + 63) / 64;
-        {
-            int per_cu = 0;
-            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, eval_lanes_kernel<16>, 1024, WL.lanes_bytes));
-            const int grid = std::min(tiles, std::max(1, per_cu) * p->num_cus);
-            hipLaunchKernelGGL(eval_lanes_kernel<16>, dim3(grid), dim3(1024), WL.lanes_bytes, st, p->dev, slot, P, scv);
-        }
-        // 8 individuals per workgroup, or 4 where 8 workspaces exceed the LDS
-        const int NWW = (size_t)kWideWG * WL.WS <= 160 * 1024 ? kWideWG : kWideWG / 2;
-        const size_t lds_w = (size_t)NWW * WL.WS;
-        auto launch_w = [&](auto kern) -> int {
-            int per_cu = 0;
-            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NWW, lds_w));
-            const int grid = (int)std::min<long>(((long)P + NWW - 1) / NWW, (long)std::max(1, per_cu) * p->num_cus);
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NWW), lds_w, st, p->dev, slot, room, P, hcv, scv,
-                               feasible, penalty, WL.BST, WL.WS, ablate);
-            return TT_OK;
-        };
-#define TT_WD(NC) \
-    case NC: rc = NWW == kWideWG ? launch_w(eval_wide_kernel<NC, kWideWG>) : launch_w(eval_wide_kernel<NC, kWideWG / 2>); break;
-        switch ((E + 255) / 256) {
-            TT_WD(1) TT_WD(2) TT_WD(3) TT_WD(4) TT_WD(5) TT_WD(6) TT_WD(7) TT_WD(8) TT_WD(9) TT_WD(10)
-            default: rc = TT_ERR_LIMIT; break;
-        }
-#undef TT_WD
-        if (rc) return rc;
-    } else if (variant >= 5 && variant <= 8) {
-        // 5/6: eval_tile5 with 4/8 waves, workspaces aliased on the tile, u32 cell
-        // counters; 7/8: tile kept for the wave phase, packed u16 counters
-        const int NW = (variant == 5 || variant == 7) ? 4 : 8;
-        const bool c32 = variant <= 6;          // u32 counters live on top of the dead tile
-        const Tile5Layout TL5 = tile5_layout(E, R, NW, c32, c32);
+    } else if (variant == 7 || variant == 8) {
+        const int NW = variant == 7 ? 4 : 8;
+        const Tile5Layout TL5 = tile5_layout(E, R, NW);
         if (p->dev.EW64 > 7 || TL5.bytes > 160 * 1024 || E > 32767) {
             set_error("instance too large for the tile5 kernel");
             return TT_ERR_LIMIT;
@@ -1394,13 +893,12 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
                                feasible, penalty, ablate);
             return TT_OK;
         };
-#define TT_T5N(EWC, NWV, C)                                                                          \
-    rc = pk == 1 ? launch(eval_tile5_kernel<EWC, NWV, C, 1, C>) : pk == 2 ? launch(eval_tile5_kernel<EWC, NWV, C, 2, C>) \
-                 : launch(eval_tile5_kernel<EWC, NWV, C, 0, C>);
+#define TT_T5U(EWC, NWV, PKV) rc = launch(eval_tile5_kernel<EWC, NWV, PKV, 1>);
+#define TT_T5N(EWC, NWV) \
+    if (pk == 1) { TT_T5U(EWC, NWV, 1) } else if (pk == 2) { TT_T5U(EWC, NWV, 2) } else { TT_T5U(EWC, NWV, 0) }
 #define TT_T5(EWC)                                                      \
     case EWC:                                                           \
-        if (NW == 4) { if (c32) { TT_T5N(EWC, 4, true) } else { TT_T5N(EWC, 4, false) } } \
-        else { if (c32) { TT_T5N(EWC, 8, true) } else { TT_T5N(EWC, 8, false) } }         \
+        if (NW == 4) { TT_T5N(EWC, 4) } else { TT_T5N(EWC, 8) }         \
         break;
         switch (p->dev.EW64) {
             TT_T5(1) TT_T5(2) TT_T5(3) TT_T5(4) TT_T5(5) TT_T5(6) TT_T5(7)
@@ -1408,6 +906,7 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
         }
 #undef TT_T5
 #undef TT_T5N
+#undef TT_T5U
         if (rc) return rc;
     } else {
         const size_t lds = block_lds_bytes(E, R);

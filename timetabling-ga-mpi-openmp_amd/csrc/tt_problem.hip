@@ -115,24 +115,7 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         stc_off[s + 1] = (int32_t)stc_ev.size();
     }
     if (stc_ev.empty()) stc_ev.assign(8, E);
-    // per-wave chunk streams for eval_tile's lane phase (students s = w mod kTileWaves)
-    std::vector<uint16_t> wch;
-    std::vector<int32_t> wch_off(kTileWaves + 1, 0);
-    if (E <= 32767) {
-        for (int w = 0; w < kTileWaves; w++) {
-            for (int s = w; s < S; s += kTileWaves) {
-                const int c0 = stc_off[s], c1 = stc_off[s + 1];
-                for (int c = c0; c < c1; c += 8) {
-                    const size_t r = wch.size();
-                    for (int j = 0; j < 8; j++) wch.push_back((uint16_t)stc_ev[c + j]);
-                    if (c + 8 == c1) wch[r] |= 0x8000;
-                }
-            }
-            wch_off[w + 1] = (int32_t)(wch.size() / 8);
-        }
-    }
-    if (wch.empty()) wch.assign(8, 0);
-    // the same records in student order, for eval_tile4: wave w of an NW-wave
+    // the lane-phase records in student order: wave w of an NW-wave
     // workgroup takes a contiguous student range, balanced by record count.
     // sch_part[sch_part_base(NW) + w] for NW = 4, 8 and 16.
     std::vector<uint16_t> sch;
@@ -183,15 +166,11 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         {ev_stu.data(), sizeof(int32_t) * ev_stu.size(), 0},
         {p->poss_bits.data(), sizeof(uint64_t) * E, 0},
         {p->corr_bits.data(), sizeof(uint32_t) * p->corr_bits.size(), 0},
-        {cp_off.data(), sizeof(int32_t) * (E + 1), 0},
-        {cp_j.data(), sizeof(int32_t) * cp_j.size(), 0},
         {nullptr, sizeof(int32_t) * 4, 0},   // status word
         {cupT.data(), sizeof(uint64_t) * cupT.size(), 0},
         {stc_off.data(), sizeof(int32_t) * stc_off.size(), 0},
         {stc_ev.data(), sizeof(int32_t) * stc_ev.size(), 0},
         {corr64.data(), sizeof(uint64_t) * corr64.size(), 0},
-        {wch.data(), sizeof(uint16_t) * wch.size(), 0},
-        {wch_off.data(), sizeof(int32_t) * wch_off.size(), 0},
         {sch.data(), sizeof(uint16_t) * sch.size(), 0},
         {sch_part.data(), sizeof(int32_t) * sch_part.size(), 0},
     };
@@ -222,18 +201,14 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     d.ev_stu = (const int32_t*)(base + parts[4].off);
     d.poss = (const uint64_t*)(base + parts[5].off);
     d.corr = (const uint32_t*)(base + parts[6].off);
-    d.cp_off = (const int32_t*)(base + parts[7].off);
-    d.cp_j = (const int32_t*)(base + parts[8].off);
-    d.status = (int32_t*)(base + parts[9].off);
+    d.status = (int32_t*)(base + parts[7].off);
     d.EW64 = EW64;
-    d.cupT = (const uint64_t*)(base + parts[10].off);
-    d.stc_off = (const int32_t*)(base + parts[11].off);
-    d.stc_ev = (const int32_t*)(base + parts[12].off);
-    d.corr64 = (const uint64_t*)(base + parts[13].off);
-    d.wch = (const uint4*)(base + parts[14].off);
-    d.wch_off = (const int32_t*)(base + parts[15].off);
-    d.sch = (const uint4*)(base + parts[16].off);
-    d.sch_part = (const int32_t*)(base + parts[17].off);
+    d.cupT = (const uint64_t*)(base + parts[8].off);
+    d.stc_off = (const int32_t*)(base + parts[9].off);
+    d.stc_ev = (const int32_t*)(base + parts[10].off);
+    d.corr64 = (const uint64_t*)(base + parts[11].off);
+    d.sch = (const uint4*)(base + parts[12].off);
+    d.sch_part = (const int32_t*)(base + parts[13].off);
     *out = p;
     return TT_OK;
 }

@@ -15,7 +15,7 @@ from ttga import native  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "med"
 P = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
-variants = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 3, 4]
+variants = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [8, 7, 13]
 inst = ttga.config_instance(cfg)
 dp = native.DeviceProblem(inst)
 seeds = torch.from_numpy(ttga.population_seeds(12345, P)).cuda()
@@ -25,7 +25,10 @@ dp.random_init(seeds, slot, room)
 ref = [t.clone() for t in dp.eval(slot, room, variant=2)]
 res = {"config": cfg, "P": P, "agree": {}, "ms_median": {}}
 for v in variants:
-    if v >> 4:                        # ablated (profiling-only) launches give invalid results
+    # ablated (profiling-only) launches give invalid results; the wide path's
+    # no-prefetch lane loop (13 | 8 << 4) does not
+    valid = {13: 8}.get(v & 15, 0)
+    if (v >> 4) & ~valid:
         continue
     got = dp.eval(slot, room, variant=v)
     res["agree"][v] = all(bool(torch.equal(a, b)) for a, b in zip(got, ref))

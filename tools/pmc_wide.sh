@@ -7,4 +7,4 @@ for c in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_SALU SQ_WAV
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d $O/pmc$i -o pmc -- python -u tools/eval_variants.py syn 65536 13 > $O/pmc$i.log 2>&1 || exit $?
 done
-python tools/pmc_summary.py $O eval_lanes_kernel > $O/lanes.json && python tools/pmc_summary.py $O eval_wide_kernel > $O/wide.json
+python tools/pmc_summary.py $O eval_lanes_kernel > $O/lanes.json && python tools/pmc_summary.py $O eval_corr_kernel > $O/corr.json
