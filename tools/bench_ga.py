@@ -16,6 +16,12 @@ population is omitted from its timing (negligible there).
 
     python tools/bench_ga.py [--config comp01] [--pop 65536] [--children 65536]
                              [--gens 3] [--steps 200] [--cpu-sample 512]
+                             [--warm-gens N] [--warm-feasible F]
+
+--warm-gens / --warm-feasible run untimed generations first, until a fraction F
+of the population is feasible (or N generations), so the timed generations
+are the GA's phase-2 regime (feasible parents, localSearch phase 2), where the
+reference spends most of a run.
 """
 import argparse
 import ctypes
@@ -35,6 +41,9 @@ import ttga  # noqa: E402
 from ttga import native  # noqa: E402
 from ttga.ga import Island  # noqa: E402
 
+sys.path.insert(0, str(REPO))
+from bench import host_cores  # noqa: E402  (every core this job may use + the CPU model)
+
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="comp01")
 ap.add_argument("--pop", type=int, default=65536)
@@ -43,6 +52,8 @@ ap.add_argument("--gens", type=int, default=3)
 ap.add_argument("--steps", type=int, default=200, help="maxSteps (-p 1: 200, -p 2: 1000, else 2000)")
 ap.add_argument("--seed", type=int, default=42)
 ap.add_argument("--cpu-sample", type=int, default=512)
+ap.add_argument("--warm-gens", type=int, default=0, help="at most this many untimed generations first")
+ap.add_argument("--warm-feasible", type=float, default=1.1, help="stop warming once this fraction is feasible")
 a = ap.parse_args()
 
 inst = ttga.config_instance(a.config)
@@ -55,6 +66,12 @@ torch.cuda.synchronize()
 init_s = time.perf_counter() - t0
 isl.step()                                  # warm-up generation
 torch.cuda.synchronize()
+warm = 1
+while warm < a.warm_gens and float(isl.pop["feasible"].float().mean().item()) < a.warm_feasible:
+    isl.step()
+    warm += 1
+feas_start = float(isl.pop["feasible"].float().mean().item())
+torch.cuda.synchronize()
 # snapshot of the population the CPU sample breeds from
 pop_slot, pop_room = isl.pop["slot"].cpu().numpy().copy(), isl.pop["room"].cpu().numpy().copy()
 pop_pen = isl.pop["penalty"].cpu().numpy().copy()
@@ -66,6 +83,7 @@ gpu_s = time.perf_counter() - t0
 feas, scv, hcv, pen = isl.member_meta(0)
 out = {"config": a.config, "E": inst.E, "R": inst.R, "F": inst.F, "S": inst.S, "pop": a.pop,
        "children_per_gen": a.children, "gens": a.gens, "max_steps": a.steps, "init_seconds": init_s,
+       "warm_gens": warm, "feasible_fraction_at_start": feas_start,
        "gpu_seconds": gpu_s, "gpu_children_per_s": a.children * a.gens / gpu_s,
        "best": {"feasible": feas, "scv": scv, "hcv": hcv, "penalty": pen},
        "feasible_fraction": float(isl.pop["feasible"].float().mean().item())}
@@ -74,7 +92,7 @@ from oracle_lib import ref  # noqa: E402
 R = ref()
 if R is not None and a.cpu_sample > 0:
     n = a.cpu_sample
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads, total, model = host_cores()
     fn = R.lib.ref_ga_children_timed
     fn.restype = ctypes.c_double
     fn.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_void_p] + [ctypes.c_int] * 4
@@ -85,7 +103,8 @@ if R is not None and a.cpu_sample > 0:
     for as_is in (0, 1):
         rng = ttga.population_seeds(777, n)
         res[as_is] = fn(h.h, P_(pop_slot), P_(pop_room), P_(pen32), a.pop, P_(rng), n, a.steps, threads, as_is)
-    out["cpu_baseline"] = {"kind": "reference", "cores": threads, "sample_children": n, "seconds": res[0],
+    out["cpu_baseline"] = {"kind": "reference", "cores": threads, "cpu_model": model, "host_cores_total": total,
+                           "sample_children": n, "seconds": res[0],
                            "children_per_s": n / res[0],
                            "what": "ga.cpp:543-577 per child (3x RandomInitialSolution, 2x selection5, copies, "
                                    "crossover into a fresh child / copy, mutation, localSearch, computePenalty), "

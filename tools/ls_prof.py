@@ -22,6 +22,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="med")
 ap.add_argument("--pop", type=int, default=4096)
 ap.add_argument("--steps", type=int, default=200)
+ap.add_argument("--pre-steps", type=int, default=0, help="untimed localSearch steps first (phase 2 start)")
 a = ap.parse_args()
 
 lib = native.load(native.PKG_DIR / "libttga_prof.so")
@@ -34,6 +35,8 @@ P, E = a.pop, inst.E
 s = torch.empty((P, E), dtype=torch.uint8, device="cuda")
 r = torch.empty_like(s)
 dp.random_init(torch.from_numpy(ttga.population_seeds(1000, P)).cuda(), s, r)
+if a.pre_steps:
+    dp.local_search(s, r, torch.from_numpy(ttga.population_seeds(5000, P)).cuda(), a.pre_steps)
 g = torch.from_numpy(ttga.population_seeds(9000, P)).cuda()
 buf = (ctypes.c_ulonglong * 16)()
 lib.tt_ls_prof_read(buf, 1)
