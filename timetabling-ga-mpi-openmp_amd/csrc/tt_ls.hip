@@ -106,6 +106,9 @@ struct LsState {
     // to the next (c1_valid) instead of being recomputed
     int c1_valid;
     int listed;          // task event lists built for the current neighbour
+    // phase 2: the state stays feasible, so every slot's rooms are distinct and
+    // hist[] is reused as the owner table oe[slot * R + room] (event, 0xFFFF free)
+    int phase2;
 #ifdef TT_LS_PROF
     uint64_t prof[kPfN];
 #endif
@@ -538,7 +541,20 @@ __device__ __forceinline__ void accept(LsState& S) {
         const int t = S.ts[k];
         for (int w = S.lane; w < S.EW; w += 64) S.B[(size_t)t * S.EW + w] = S.NB[(size_t)k * S.EW + w];
         const LsTask T = get_task(S, k);
-        for (int r = S.lane; r < S.R; r += 64) S.hist[t * S.R + r] = T.hist[r];
+        for (int r = S.lane; r < S.R; r += 64) S.hist[t * S.R + r] = S.phase2 ? (uint16_t)0xFFFF : T.hist[r];
+    }
+    if (S.phase2) {                   // owner table rows of the touched slots, from the new rooms
+        wave_sync();
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (k >= S.nts) break;
+            const int t = S.ts[k];
+            for (int w = S.lane; w < S.EW; w += 64)
+                for (uint64_t x = S.NB[(size_t)k * S.EW + w]; x; x &= x - 1) {
+                    const int e = 64 * w + __builtin_ctzll(x);
+                    S.hist[t * S.R + S.rr[e]] = (uint16_t)e;
+                }
+        }
     }
     if (S.lane == 0) {
 #pragma unroll
@@ -596,6 +612,94 @@ __device__ __forceinline__ bool feasible_now(LsState& S) {
     return f;
 }
 
+// ---- correlation shortcuts. Phase 1 (Solution.cpp:497-618): the visited
+// event's row and X[t] give corr_nb(ei) of a Move1 to t and of a Move2 with an
+// event of t without reading the row again; a Move2 partner's row is loaded
+// once per trial (one trial ahead) and its two counts share one reduction, so
+// the lower bound rejects most trials before any neighbour is built.
+// Phase-2 shortcuts (Solution.cpp:619-768). In phase 2 the state is
+// feasible and only moves with eventAffectedHcv == 0 for every moved event are
+// accepted, so a trial is rejected, before any neighbour is built, when
+//  * a moved event meets a correlated event in its new slot (the count of the
+//    visited event's correlated events per slot, X[t], and the OR of its
+//    slot-mates' correlation rows, Z, are computed once per visit), or
+//  * a touched slot cannot be room-matched without a clash: the reference's
+//    assignRooms gives zero clash pairs exactly when a perfect matching exists
+//    (it is a maximum matching, and an unmatched event has no free possible
+//    room), and a perfect one exists exactly when the moved-in event has an
+//    augmenting path from the slot's current (clash-free) rooms.
+// The RNG draws are the reference's; every other trial takes the full path.
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+// bit e of a row held one 64-bit word per lane
+__device__ __forceinline__ bool row_bit(uint64_t lane_words, int e) {
+    return (readlane64(lane_words, e >> 6) >> (e & 63)) & 1ull;
+}
+
+struct Visit2 {
+    uint64_t row;     // lane w: word w of corr64[ei]
+    uint64_t z;       // lane w: word w of the OR of corr64[k], k in slot(ei), k != ei
+    int x;            // lane t: popcount(corr64[ei] & B[t])
+};
+
+__device__ __forceinline__ void visit2_row_x(LsState& S, int ei, Visit2& V) {
+    const int EW = S.EW, lane = S.lane;
+    V.row = lane < EW ? S.pb.corr64[(size_t)ei * EW + lane] : 0ull;
+    int x = 0;
+    for (int w = 0; w < EW; ++w) {
+        const uint64_t rw = readlane64(V.row, w);
+        if (lane < kSlots) x += __popcll(rw & S.B[(size_t)lane * EW + w]);
+    }
+    V.x = x;
+}
+
+__device__ __forceinline__ void visit2_z(LsState& S, int ei, Visit2& V) {
+    const int EW = S.EW, lane = S.lane, ti = S.sl[ei];
+    uint64_t z = 0;
+    for (int w2 = 0; w2 < EW; ++w2) {
+        const uint64_t bw = S.B[(size_t)ti * EW + w2];
+        uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(bw >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bw);
+        if ((ei >> 6) == w2) m &= ~(1ull << (ei & 63));
+        while (m) {
+            const int k = 64 * w2 + __builtin_ctzll(m);
+            m &= m - 1;
+            if (lane < EW) z |= S.pb.corr64[(size_t)k * EW + lane];
+        }
+    }
+    V.z = z;
+}
+
+// sum over words of popcount(row & set) for a row held one word per lane (lanes < EW)
+__device__ __forceinline__ int row_in_set(const LsState& S, uint64_t row, const uint64_t* set) {
+    return wave_sum(S.lane < S.EW ? __popcll(row & set[S.lane]) : 0);
+}
+
+// Slot s minus event `out` (-1: none) plus event `a` has a clash-free room
+// matching (an augmenting path from `a` over the owner table).
+__device__ __forceinline__ bool matchable(LsState& S, int s, int out, int a) {
+    const int R = S.R, lane = S.lane;
+    const int o = lane < R ? (int)S.hist[s * R + lane] : 0xFFFF;
+    const bool valid = o != 0xFFFF && o != out;
+    const uint64_t po = valid ? S.pb.poss[o] : 0ull;
+    const uint64_t used = __ballot(valid);
+    const uint64_t fre = (R >= 64 ? ~0ull : ((1ull << R) - 1)) & ~used;
+    uint64_t seen = S.pb.poss[a];
+    if (seen & fre) return true;
+    uint64_t fr = seen & used;
+    while (fr) {
+        const int r = __builtin_ctzll(fr);
+        fr &= fr - 1;
+        const uint64_t nx = readlane64(po, r) & ~seen;
+        if (nx & fre) return true;
+        seen |= nx;
+        fr |= nx & used;
+    }
+    return false;
+}
+
 // CAP = matcher task capacity. redo_out (first launch): set to 1 for an
 // individual that overflowed a task, whose HBM row and stream are then left
 // as they were. redo_in (second launch): only flagged individuals run.
@@ -626,6 +730,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
     S.nmv = 0; S.nts = 0;
     S.c1_valid = 0;
     S.listed = 0;
+    S.phase2 = 0;
 #ifdef TT_LS_PROF
 #pragma unroll
     for (int i = 0; i < kPfN; ++i) S.prof[i] = 0;
@@ -693,30 +798,36 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
     // tests/test_gpu_parity.py asserts it never fires.
     const long guard_max = 4l * (long)E * ((long)max_steps + 2) + 1024;
     long guard = 0;
+    const bool fast1 = EW <= 64;                                        // row words fit the lanes
     if (!feasible_now(S)) {                                             // phase 1 (Solution.cpp:497-618)
         for (int i = 0; evc < E; i = (i + 1) % E) {
             if (step > max_steps || ++guard > guard_max) break;
             const int ei = S.evl[i];
             LSP_CNT(S, kPfVisits);
             if (ehcv_cur(S, ei) == 0) { evc++; continue; }
+            const int t_orig = S.sl[ei];
+            Visit2 V;
+            if (fast1) visit2_row_x(S, ei, V);
             // eventAffectedHcv(ei) in the current state: unchanged until a trial is
             // accepted, and every acceptance leaves this event's loops
-            const int eah_i = eah_cur(S, ei);
+            const int eah_i = fast1 ? S.rp[t_orig] + __builtin_amdgcn_readlane(V.x, t_orig) - (int)row_bit(V.row, ei)
+                                    : eah_cur(S, ei);
             const int t_start = pm_pick(st, kSlots);
-            const int t_orig = S.sl[ei];
             for (int h = 0, t = t_start; h < kSlots; t = (t + 1) % kSlots, h++) {
                 if (step > max_steps) break;
                 if (pm_next(st) < p1) {
                     step++;
+                    const int c = eah_i + S.rp[t];
+                    // the kept old-slot task gives misc[1]; corr_nb(ei) in t is X[t]
+                    if (fast1 && S.c1_valid && t != t_orig && __builtin_amdgcn_readlane(V.x, t) + S.misc[1] >= c) continue;
                     set_move(S, 1, ei, t, 0);
                     build_nb(S);
-                    const int c = eah_i + S.rp[t];
                     if (S.nts == 2) {
                         // task 0 = t plus ei, task 1 = t_orig minus ei (kept across trials).
                         // n = corr + misc[1] + misc[0] >= corr + misc[1]: a trial that cannot
                         // win is rejected before the target slot is matched.
                         if (match_tasks(S, 2)) goto redo;
-                        const int lb = corr_nb(S, ei) + S.misc[1];
+                        const int lb = (fast1 ? __builtin_amdgcn_readlane(V.x, t) : corr_nb(S, ei)) + S.misc[1];
                         if (lb >= c) { S.c1_valid = 1; continue; }
                         if (match_tasks(S, 1)) goto redo;
                         if (lb + S.misc[0] < c) { accept(S); evc = 0; better = true; break; }
@@ -731,16 +842,53 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
             cache_drop(S);
             if (better) { better = false; continue; }
             if (p2 != 0) {
+                // B[t_orig] without ei: the partner's slot-mates after a swap
+                uint64_t bo = 0;
+                if (fast1 && lane < EW) {
+                    bo = S.B[(size_t)t_orig * EW + lane];
+                    if ((ei >> 6) == lane) bo &= ~(1ull << (ei & 63));
+                }
+                // partners' rows two trials ahead: (e, row) of trials j and j+1 in flight
+                int pe0 = -1, pe1 = -1;
+                uint64_t pr0 = 0, pr1 = 0;
+                auto fetch = [&](int jj, int& pe, uint64_t& pr) {
+                    pe = jj == i ? -1 : S.evl[jj];
+                    pr = (pe >= 0 && lane < EW) ? S.pb.corr64[(size_t)pe * EW + lane] : 0ull;
+                };
+                if (fast1) {
+                    fetch((i + 1) % E, pe0, pr0);
+                    fetch((i + 2) % E, pe1, pr1);
+                }
                 for (int j = (i + 1) % E; j != i; j = (j + 1) % E) {
                     if (step > max_steps) break;
+                    const uint64_t rj = pr0;
+                    if (fast1) {
+                        pe0 = pe1; pr0 = pr1;
+                        if (pe1 >= 0) fetch((j + 2) % E, pe1, pr1);
+                    }
                     if (pm_next(st) < p2) {
                         step++;
                         const int ej = S.evl[j];
-                        const int c = eah_i + eah_cur(S, ej);
-                        set_move(S, 2, ei, ej, 0);
-                        build_nb(S);
-                        const int lb = corr_nb(S, ei) + corr_nb(S, ej);    // n >= lb whatever the rooms
-                        if (lb >= c) continue;
+                        int c, lb;
+                        const int tj = S.sl[ej];
+                        if (fast1 && tj != t_orig) {
+                            // eah_cur(ej) = rp[tj] + |corr(ej) & B[tj]| - corr(ej,ej);
+                            // corr_nb(ei) = X[tj] - corr(ei,ej); corr_nb(ej) = |corr(ej) & (B[t_orig] - ei)|
+                            const int both = wave_sum(lane < EW ? __popcll(rj & S.B[(size_t)tj * EW + lane]) |
+                                                                      (__popcll(rj & bo) << 16) : 0);
+                            const int cij = (int)row_bit(V.row, ej);
+                            c = eah_i + S.rp[tj] + (both & 0xFFFF) - (int)row_bit(rj, ej);
+                            lb = __builtin_amdgcn_readlane(V.x, tj) - cij + (both >> 16);
+                            if (lb >= c) continue;
+                            set_move(S, 2, ei, ej, 0);
+                            build_nb(S);
+                        } else {
+                            c = eah_i + eah_cur(S, ej);
+                            set_move(S, 2, ei, ej, 0);
+                            build_nb(S);
+                            lb = corr_nb(S, ei) + corr_nb(S, ej);    // n >= lb whatever the rooms
+                            if (lb >= c) continue;
+                        }
                         const TaskRegs tr = load_tasks(S, 7);
                         if (S.nts == 2) {             // task 0 = slot(ej) plus ei, task 1 = slot(ei) plus ej
                             if (match_tasks(S, 1, tr)) goto redo;
@@ -788,6 +936,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
         }
     }
     if (feasible_now(S)) {                                              // phase 2 (Solution.cpp:619-768)
+        // owner table in place of the room histogram (rooms are distinct per slot now)
+        S.phase2 = 1;
+        for (int c = lane; c < kSlots * R; c += 64) S.hist[c] = 0xFFFF;
+        wave_sync();
+        for (int e = lane; e < E; e += 64) S.hist[S.sl[e] * R + S.rr[e]] = (uint16_t)e;
+        wave_sync();
+        const bool fast = fast1;
         evc = 0;
         for (int i = 0; evc < E; i = (i + 1) % E) {
             if (step > max_steps || ++guard > guard_max) break;
@@ -796,17 +951,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
             int cur, scs_i;
             scv_terms(S, ei, false, cur, scs_i);
             if (cur == 0) { evc++; continue; }
+            const int ti = S.sl[ei];
+            Visit2 V;
+            if (fast) visit2_row_x(S, ei, V);
             const int t_start = pm_pick(st, kSlots);
             for (int h = 0, t = t_start; h < kSlots; t = (t + 1) % kSlots, h++) {
                 if (step > max_steps) break;
                 if (pm_next(st) < p1) {
                     step++;
+                    if (fast && t != ti) {
+                        // ei meets a correlated event in t, or t cannot take ei without a clash
+                        if (__builtin_amdgcn_readlane(V.x, t) != 0) continue;
+                        if (!matchable(S, t, -1, ei)) continue;
+                    }
                     set_move(S, 1, ei, t, 0);
                     build_nb(S);
                     // eah_nb(ei) == 0 needs no correlated event in t (no rooms needed)
                     // and no room clash in t (task 0); the old slot (task 1) is
                     // matched only for an accepted move
-                    if (corr_nb(S, ei) != 0) continue;
+                    if (!(fast && t != ti) && corr_nb(S, ei) != 0) continue;
                     if (match_tasks(S, 1)) goto redo;
                     if (S.misc[0] == 0) {
                         int es_n, scs_n;
@@ -822,14 +985,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
             cache_drop(S);
             if (better) { better = false; continue; }
             if (p2 != 0) {
+                if (fast) visit2_z(S, ei, V);
                 for (int j = (i + 1) % E; j != i; j = (j + 1) % E) {
                     if (step > max_steps) break;
                     if (pm_next(st) < p2) {
                         step++;
                         const int ej = S.evl[j];
+                        const int tj = S.sl[ej];
+                        const bool quick = fast && tj != ti;
+                        if (quick) {
+                            // corr_nb(ei) = X[tj] - corr(ei, ej); corr_nb(ej) = 0 iff no slot-mate of ei
+                            // is correlated with ej; then both slots must match without a clash
+                            if (__builtin_amdgcn_readlane(V.x, tj) - (int)row_bit(V.row, ej) != 0) continue;
+                            if (row_bit(V.z, ej)) continue;
+                            if (!matchable(S, tj, ej, ei) || !matchable(S, ti, ei, ej)) continue;
+                        }
                         set_move(S, 2, ei, ej, 0);
                         build_nb(S);
-                        if (corr_nb(S, ei) + corr_nb(S, ej) != 0) continue;   // eah_nb > 0 whatever the rooms
+                        if (!quick && corr_nb(S, ei) + corr_nb(S, ej) != 0) continue;   // eah_nb > 0 whatever the rooms
                         const TaskRegs tr = load_tasks(S, 7);
                         if (S.nts == 2) {
                             if (match_tasks(S, 1, tr)) goto redo;

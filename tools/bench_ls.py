@@ -62,7 +62,7 @@ out = {"config": a.config, "pop": P, "max_steps": a.steps, "pre_steps": a.pre_st
        "mean_penalty": float(pen.double().mean())}
 from oracle_lib import ref  # noqa: E402
 R = ref()
-if R is not None:
+if R is not None and a.cpu_sample > 0:
     n = min(a.cpu_sample, P)
     ss, rr, gg = s0[:n].cpu().numpy().copy(), r0[:n].cpu().numpy().copy(), lseeds[:n].cpu().numpy().copy()
     threads, total, model = host_cores()
