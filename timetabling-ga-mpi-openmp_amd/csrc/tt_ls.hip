@@ -33,7 +33,7 @@ constexpr int kLsCapSmall = 64;
 // Profiling build (-DTT_LS_PROF, `make libttga_prof.so`, tools/ls_prof.py):
 // per-section shader-clock totals of every wave, summed into g_ls_prof.
 #ifdef TT_LS_PROF
-enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfN };
+enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfQ1, kPfQ1c, kPfQ1m, kPfQ2, kPfQ2c, kPfQ2m, kPfP1m2, kPfP1m2lb, kPfMaxTotal, kPfN };
 __device__ unsigned long long g_ls_prof[kPfN];
 #define LSP_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define LSP_ADD(St, i, v) ((St).prof[i] += __builtin_amdgcn_s_memtime() - (v))
@@ -700,6 +700,61 @@ __device__ __forceinline__ bool matchable(LsState& S, int s, int out, int a) {
     return false;
 }
 
+// ---- trial windows. A Move1/Move2 loop spends most of its trials on moves
+// the cheap tests above reject. Up to 64 consecutive trials are screened at
+// once, one per lane: lane k takes the trial k+1 draws ahead (Park-Miller jump:
+// state * 16807^(k+1) mod (2^31 - 1), the exact value of k+1 Schrage steps),
+// its draw, and whether it needs the full path; the step budget is applied
+// as the scalar loop does (a trial runs only while step <= maxSteps, and only
+// a passing draw costs a step). The first lane that needs the full path is
+// run by the scalar code; the trials before it were rejected with their draws
+// and steps consumed, exactly as one by one.
+constexpr uint32_t kPmM = 2147483647u;
+__device__ __forceinline__ uint32_t pm_mulmod(uint32_t a, uint32_t b) {
+    const uint64_t p = (uint64_t)a * b;
+    const uint32_t r = (uint32_t)(p & kPmM) + (uint32_t)(p >> 31);
+    return r >= kPmM ? r - kPmM : r;
+}
+// 16807^(n) mod (2^31 - 1)
+__device__ __forceinline__ uint32_t pm_pow(int n) {
+    uint32_t r = 1, b = 16807u;
+    for (; n; n >>= 1) {
+        if (n & 1) r = pm_mulmod(r, b);
+        b = pm_mulmod(b, b);
+    }
+    return r;
+}
+__device__ __forceinline__ int bperm(int v, int src_lane) { return __builtin_amdgcn_ds_bpermute(src_lane << 2, v); }
+__device__ __forceinline__ uint64_t bperm64(uint64_t v, int src_lane) {
+    return ((uint64_t)(uint32_t)bperm((int)(uint32_t)(v >> 32), src_lane) << 32) | (uint32_t)bperm((int)(uint32_t)v, src_lane);
+}
+
+// Resolves a window of `rem` remaining trials (lanes k < rem) whose per-lane
+// full-path flag is `need`: returns the lane of the first trial to run in
+// full (64: none), with st/step advanced past it (its draw and step taken);
+// without one, past every trial the loop would have run, and done is set when
+// the loop ends inside the window (step budget or its last trial).
+__device__ __forceinline__ int window_resolve(int lane, uint32_t jump, int64_t& st, int& step, int max_steps, int rem,
+                                              double p, bool need, bool& done) {
+    const uint32_t sk = pm_mulmod((uint32_t)st, jump);
+    const bool valid = lane < rem;
+    const bool d = valid && __dmul_rn(1.0 / 2147483647.0, (double)sk) < p;
+    const uint64_t dm = __ballot(d);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const bool alive = valid && step + __popcll(dm & lt) <= max_steps;
+    const uint64_t am = __ballot(alive);
+    const int kend = am == ~0ull ? 64 : __builtin_ctzll(~am);
+    const uint64_t nm = __ballot(alive && d && need);
+    const int kstar = nm ? __builtin_ctzll(nm) : 64;
+    const int last = kstar < 64 ? kstar : kend - 1;                    // last trial drawn
+    if (last >= 0) {
+        st = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)sk, last);
+        step += __popcll(dm & (last == 63 ? ~0ull : ((2ull << last) - 1ull)));
+    }
+    done = kstar == 64 && (kend < 64 || rem <= 64);
+    return kstar;
+}
+
 // CAP = matcher task capacity. redo_out (first launch): set to 1 for an
 // individual that overflowed a task, whose HBM row and stream are then left
 // as they were. redo_in (second launch): only flagged individuals run.
@@ -736,6 +791,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
     for (int i = 0; i < kPfN; ++i) S.prof[i] = 0;
 #endif
     if (lane == 0) S.misc[3] = 0;
+    const uint32_t jump = pm_pow(lane + 1);                             // lane k: k+1 draws ahead
 
     // ---- load the individual, derive the incremental state
     bool bad = false;
@@ -848,57 +904,65 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                     bo = S.B[(size_t)t_orig * EW + lane];
                     if ((ei >> 6) == lane) bo &= ~(1ull << (ei & 63));
                 }
-                // partners' rows two trials ahead: (e, row) of trials j and j+1 in flight
-                int pe0 = -1, pe1 = -1;
-                uint64_t pr0 = 0, pr1 = 0;
-                auto fetch = [&](int jj, int& pe, uint64_t& pr) {
-                    pe = jj == i ? -1 : S.evl[jj];
-                    pr = (pe >= 0 && lane < EW) ? S.pb.corr64[(size_t)pe * EW + lane] : 0ull;
-                };
-                if (fast1) {
-                    fetch((i + 1) % E, pe0, pr0);
-                    fetch((i + 2) % E, pe1, pr1);
-                }
-                for (int j = (i + 1) % E; j != i; j = (j + 1) % E) {
+                int j = (i + 1) % E;
+                while (j != i) {
                     if (step > max_steps) break;
-                    const uint64_t rj = pr0;
-                    if (fast1) {
-                        pe0 = pe1; pr0 = pr1;
-                        if (pe1 >= 0) fetch((j + 2) % E, pe1, pr1);
-                    }
-                    if (pm_next(st) < p2) {
-                        step++;
-                        const int ej = S.evl[j];
-                        int c, lb;
-                        const int tj = S.sl[ej];
-                        if (fast1 && tj != t_orig) {
-                            // eah_cur(ej) = rp[tj] + |corr(ej) & B[tj]| - corr(ej,ej);
-                            // corr_nb(ei) = X[tj] - corr(ei,ej); corr_nb(ej) = |corr(ej) & (B[t_orig] - ei)|
-                            const int both = wave_sum(lane < EW ? __popcll(rj & S.B[(size_t)tj * EW + lane]) |
-                                                                      (__popcll(rj & bo) << 16) : 0);
-                            const int cij = (int)row_bit(V.row, ej);
-                            c = eah_i + S.rp[tj] + (both & 0xFFFF) - (int)row_bit(rj, ej);
-                            lb = __builtin_amdgcn_readlane(V.x, tj) - cij + (both >> 16);
-                            if (lb >= c) continue;
-                            set_move(S, 2, ei, ej, 0);
-                            build_nb(S);
-                        } else {
-                            c = eah_i + eah_cur(S, ej);
-                            set_move(S, 2, ei, ej, 0);
-                            build_nb(S);
-                            lb = corr_nb(S, ei) + corr_nb(S, ej);    // n >= lb whatever the rooms
-                            if (lb >= c) continue;
+                    if (fast1 && (uint64_t)st < kPmM) {
+                        // window: lane k screens trial j+k against the lower bound
+                        // lb = corr_nb(ei) + corr_nb(ej) >= c = eah_i + eah_cur(ej)
+                        const int rem = (i - j + E) % E;
+                        // (ds_bpermute reads 0 from inactive lanes: every lane takes part)
+                        const int ej = S.evl[(j + lane) % E], tj = S.sl[ej];
+                        const int xt = bperm(V.x, tj);
+                        bool need = true;
+                        if (lane < rem && tj != t_orig) {
+                            int c1 = 0, c2 = 0, selfj = 0, cij = 0;
+                            for (int w = 0; w < EW; ++w) {
+                                const uint64_t rw = S.pb.corr64[(size_t)ej * EW + w];
+                                c1 += __popcll(rw & S.B[(size_t)tj * EW + w]);
+                                c2 += __popcll(rw & readlane64(bo, w));
+                                if (w == (ej >> 6)) selfj = (int)((rw >> (ej & 63)) & 1ull);
+                                if (w == (ei >> 6)) cij = (int)((rw >> (ei & 63)) & 1ull);
+                            }
+                            const int c = eah_i + S.rp[tj] + c1 - selfj;
+                            const int lb = xt - cij + c2;
+                            need = lb < c;
                         }
+                        bool done;
+                        const int ks = window_resolve(lane, jump, st, step, max_steps, rem, p2, need, done);
+                        if (ks == 64) {
+                            if (done) break;
+                            j = (j + 64) % E;
+                            continue;
+                        }
+                        j = (j + ks) % E;
+                    } else {
+                        if (!(pm_next(st) < p2)) { j = (j + 1) % E; continue; }
+                        step++;
+                    }
+                    // ---- the full trial at j (its draw and step taken)
+                    bool acc = false;
+                    do {
+                        const int ej = S.evl[j];
+                        const int c = eah_i + eah_cur(S, ej);
+                        set_move(S, 2, ei, ej, 0);
+                        build_nb(S);
+                        const int lb = corr_nb(S, ei) + corr_nb(S, ej);    // n >= lb whatever the rooms
+                        LSP_CNT(S, kPfP1m2);
+                        if (lb >= c) break;
+                        LSP_CNT(S, kPfP1m2lb);
                         const TaskRegs tr = load_tasks(S, 7);
                         if (S.nts == 2) {             // task 0 = slot(ej) plus ei, task 1 = slot(ei) plus ej
                             if (match_tasks(S, 1, tr)) goto redo;
-                            if (lb + S.misc[0] >= c) { restore_task<0>(S); continue; }
+                            if (lb + S.misc[0] >= c) { restore_task<0>(S); break; }
                             if (match_tasks(S, 2, tr)) goto redo;
                         } else if (match_tasks(S, 7, tr)) goto redo;
                         const int n = lb + S.misc[task_of(S, slot_nb(S, ei))] + S.misc[task_of(S, slot_nb(S, ej))];
-                        if (n < c) { accept(S); evc = 0; better = true; break; }
+                        if (n < c) { accept(S); acc = true; break; }
                         sync_rooms(S, false);
-                    }
+                    } while (0);
+                    if (acc) { evc = 0; better = true; break; }
+                    j = (j + 1) % E;
                 }
                 if (better) { better = false; continue; }
             }
@@ -955,58 +1019,105 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
             Visit2 V;
             if (fast) visit2_row_x(S, ei, V);
             const int t_start = pm_pick(st, kSlots);
-            for (int h = 0, t = t_start; h < kSlots; t = (t + 1) % kSlots, h++) {
+            for (int h = 0; h < kSlots;) {
                 if (step > max_steps) break;
-                if (pm_next(st) < p1) {
+                const bool win = fast && (uint64_t)st < kPmM;
+                if (win) {
+                    // window: lane k screens target t_start+h+k (ei must meet no correlated event there)
+                    const int rem = kSlots - h;
+                    const int tk = (t_start + h + lane) % kSlots;
+                    const int xt = bperm(V.x, tk);                          // every lane takes part
+                    const bool need = lane < rem && (tk == ti || xt == 0);
+                    bool done;
+                    const int ks = window_resolve(lane, jump, st, step, max_steps, rem, p1, need, done);
+                    if (ks == 64) break;                                // rem <= 45 < 64: the loop ends here
+                    h += ks;
+                } else {
+                    if (!(pm_next(st) < p1)) { h++; continue; }
                     step++;
-                    if (fast && t != ti) {
-                        // ei meets a correlated event in t, or t cannot take ei without a clash
-                        if (__builtin_amdgcn_readlane(V.x, t) != 0) continue;
-                        if (!matchable(S, t, -1, ei)) continue;
-                    }
-                    set_move(S, 1, ei, t, 0);
-                    build_nb(S);
-                    // eah_nb(ei) == 0 needs no correlated event in t (no rooms needed)
-                    // and no room clash in t (task 0); the old slot (task 1) is
-                    // matched only for an accepted move
-                    if (!(fast && t != ti) && corr_nb(S, ei) != 0) continue;
-                    if (match_tasks(S, 1)) goto redo;
-                    if (S.misc[0] == 0) {
-                        int es_n, scs_n;
-                        scv_terms(S, ei, true, es_n, scs_n);
-                        if (es_n + scs_i - scs_n < cur) {
-                            if (match_tasks(S, 2)) goto redo;
-                            accept(S); evc = 0; better = true; break;
-                        }
-                    }
-                    restore_task<0>(S);
                 }
+                const int t = (t_start + h) % kSlots;
+                h++;
+                if (fast && t != ti) {
+                    // ei meets a correlated event in t, or t cannot take ei without a clash
+                    LSP_CNT(S, kPfQ1);
+                    if (__builtin_amdgcn_readlane(V.x, t) != 0) continue;
+                    LSP_CNT(S, kPfQ1c);
+                    if (!matchable(S, t, -1, ei)) continue;
+                    LSP_CNT(S, kPfQ1m);
+                }
+                set_move(S, 1, ei, t, 0);
+                build_nb(S);
+                // eah_nb(ei) == 0 needs no correlated event in t (no rooms needed)
+                // and no room clash in t (task 0); the old slot (task 1) is
+                // matched only for an accepted move
+                if (!(fast && t != ti) && corr_nb(S, ei) != 0) continue;
+                if (match_tasks(S, 1)) goto redo;
+                if (S.misc[0] == 0) {
+                    int es_n, scs_n;
+                    scv_terms(S, ei, true, es_n, scs_n);
+                    if (es_n + scs_i - scs_n < cur) {
+                        if (match_tasks(S, 2)) goto redo;
+                        accept(S); evc = 0; better = true; break;
+                    }
+                }
+                restore_task<0>(S);
             }
             cache_drop(S);
             if (better) { better = false; continue; }
             if (p2 != 0) {
                 if (fast) visit2_z(S, ei, V);
-                for (int j = (i + 1) % E; j != i; j = (j + 1) % E) {
+                int j = (i + 1) % E;
+                while (j != i) {
                     if (step > max_steps) break;
-                    if (pm_next(st) < p2) {
+                    if (fast && (uint64_t)st < kPmM) {
+                        // window: lane k screens partner j+k (no correlated event for either
+                        // moved event in its new slot)
+                        const int rem = (i - j + E) % E;
+                        // (ds_bpermute reads 0 from inactive lanes: every lane takes part)
+                        const int ej = S.evl[(j + lane) % E], tj = S.sl[ej];
+                        const uint64_t rw = bperm64(V.row, ej >> 6), zw = bperm64(V.z, ej >> 6);
+                        const int xt = bperm(V.x, tj);
+                        bool need = true;
+                        if (lane < rem && tj != ti) {
+                            const int cij = (int)((rw >> (ej & 63)) & 1ull);
+                            need = xt - cij == 0 && !((zw >> (ej & 63)) & 1ull);
+                        }
+                        bool done;
+                        const int ks = window_resolve(lane, jump, st, step, max_steps, rem, p2, need, done);
+                        if (ks == 64) {
+                            if (done) break;
+                            j = (j + 64) % E;
+                            continue;
+                        }
+                        j = (j + ks) % E;
+                    } else {
+                        if (!(pm_next(st) < p2)) { j = (j + 1) % E; continue; }
                         step++;
+                    }
+                    // ---- the full trial at j (its draw and step taken)
+                    bool acc = false;
+                    do {
                         const int ej = S.evl[j];
                         const int tj = S.sl[ej];
                         const bool quick = fast && tj != ti;
                         if (quick) {
                             // corr_nb(ei) = X[tj] - corr(ei, ej); corr_nb(ej) = 0 iff no slot-mate of ei
                             // is correlated with ej; then both slots must match without a clash
-                            if (__builtin_amdgcn_readlane(V.x, tj) - (int)row_bit(V.row, ej) != 0) continue;
-                            if (row_bit(V.z, ej)) continue;
-                            if (!matchable(S, tj, ej, ei) || !matchable(S, ti, ei, ej)) continue;
+                            LSP_CNT(S, kPfQ2);
+                            if (__builtin_amdgcn_readlane(V.x, tj) - (int)row_bit(V.row, ej) != 0) break;
+                            if (row_bit(V.z, ej)) break;
+                            LSP_CNT(S, kPfQ2c);
+                            if (!matchable(S, tj, ej, ei) || !matchable(S, ti, ei, ej)) break;
+                            LSP_CNT(S, kPfQ2m);
                         }
                         set_move(S, 2, ei, ej, 0);
                         build_nb(S);
-                        if (!quick && corr_nb(S, ei) + corr_nb(S, ej) != 0) continue;   // eah_nb > 0 whatever the rooms
+                        if (!quick && corr_nb(S, ei) + corr_nb(S, ej) != 0) break;   // eah_nb > 0 whatever the rooms
                         const TaskRegs tr = load_tasks(S, 7);
                         if (S.nts == 2) {
                             if (match_tasks(S, 1, tr)) goto redo;
-                            if (S.misc[0] != 0) { restore_task<0>(S); continue; }
+                            if (S.misc[0] != 0) { restore_task<0>(S); break; }
                             if (match_tasks(S, 2, tr)) goto redo;
                         } else if (match_tasks(S, 7, tr)) goto redo;
                         if (S.misc[task_of(S, slot_nb(S, ei))] + S.misc[task_of(S, slot_nb(S, ej))] == 0) {
@@ -1015,10 +1126,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                             scv_terms(S, ej, true, es_nj, scs_nj);
                             scv_terms(S, ej, false, es_cj, scs_cj);
                             const int n = es_ni + scs_i - scs_ni + es_nj + scs_cj - scs_nj;
-                            if (n < cur + es_cj) { accept(S); evc = 0; better = true; break; }
+                            if (n < cur + es_cj) { accept(S); acc = true; break; }
                         }
                         sync_rooms(S, false);
-                    }
+                    } while (0);
+                    if (acc) { evc = 0; better = true; break; }
+                    j = (j + 1) % E;
                 }
                 if (better) { better = false; continue; }
             }
@@ -1069,7 +1182,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
     LSP_CNT(S, kPfWaves);
     if (lane == 0) {
 #pragma unroll
-        for (int i = 0; i < kPfN; ++i) atomicAdd(&g_ls_prof[i], (unsigned long long)S.prof[i]);
+        for (int i = 0; i < kPfMaxTotal; ++i) atomicAdd(&g_ls_prof[i], (unsigned long long)S.prof[i]);
+        atomicMax(&g_ls_prof[kPfMaxTotal], (unsigned long long)S.prof[kPfTotal]);   // the slowest wave
     }
 #endif
     return;

@@ -16,7 +16,9 @@ import ttga  # noqa: E402
 from ttga import native  # noqa: E402
 
 NAMES = ["init", "build_and_match", "match_task_wave", "corr_in_set", "scv_terms", "sync_accept", "feasible_now",
-         "total", "trials", "event_visits", "waves", "scramble", "match_calls", "match_events", "match_steps"]
+         "total", "trials", "event_visits", "waves", "scramble", "match_calls", "match_events", "match_steps",
+         "p2_move1", "p2_move1_corr_ok", "p2_move1_match_ok", "p2_move2", "p2_move2_corr_ok", "p2_move2_match_ok",
+         "p1_move2_quick", "p1_move2_lb_ok", "max_total"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="med")
@@ -38,7 +40,7 @@ dp.random_init(torch.from_numpy(ttga.population_seeds(1000, P)).cuda(), s, r)
 if a.pre_steps:
     dp.local_search(s, r, torch.from_numpy(ttga.population_seeds(5000, P)).cuda(), a.pre_steps)
 g = torch.from_numpy(ttga.population_seeds(9000, P)).cuda()
-buf = (ctypes.c_ulonglong * 16)()
+buf = (ctypes.c_ulonglong * 32)()
 lib.tt_ls_prof_read(buf, 1)
 dp.local_search(s, r, g, a.steps)
 torch.cuda.synchronize()
@@ -49,6 +51,7 @@ out = {"config": a.config, "pop": P, "max_steps": a.steps, "raw": v,
        "cycles_per_trial": {k: v[k] / trials for k in NAMES[:7]},
        "cycles_per_wave": {k: v[k] / waves for k in NAMES[:8] + ["scramble"]},
        "trials_per_wave": v["trials"] / waves, "visits_per_wave": v["event_visits"] / waves,
+       "slowest_wave_cycles": v["max_total"], "slowest_over_mean": v["max_total"] / max(v["total"] / waves, 1),
        "note": "s_memtime deltas summed over waves that finished in the first launch; sections nest "
                "(match_task_wave and corr_in_set inside build_and_match/deltas)"}
 print(json.dumps(out, indent=1))
