@@ -325,3 +325,28 @@ def test_rng_edge_seeds_vs_oracle(orc):
     dp.local_search(s, r, g, 300)
     ls, lr, lg = o.local_search(es, er, seeds.copy(), 300)
     assert np.array_equal(host(s), ls) and np.array_equal(host(r), lr) and np.array_equal(host(g), lg)
+
+
+@pytest.mark.parametrize("dims,p1,p2", [((50, 5, 4, 40), 1.0, 1.0), ((120, 6, 4, 90), 0.9, 0.35)],
+                         ids=["E50", "E120_p"])
+def test_local_search_step_budget_windows(orc, dims, p1, p2):
+    """The local search screens up to 64 trials per pass (one per lane, with
+    Park-Miller jump-ahead draws) and must stop exactly where the reference's
+    step budget stops it: many small maxSteps values, so the budget runs out
+    inside a window at every offset, from random init (phase 1) and from
+    mostly feasible individuals (phase 2); E < 64 (windows wrapping the event
+    ring more than once) and draw probabilities below 1."""
+    inst = ttga.generate(*dims, seed=19)
+    dp = native.DeviceProblem(inst)
+    o = orc.problem(inst)
+    P = 16
+    s0, r0, _ = o.random_init(ttga.population_seeds(2101, P))
+    f_s, f_r, _ = o.local_search(s0, r0, ttga.population_seeds(2201, P), 4000, p1, p2)
+    for start_s, start_r in ((s0, r0), (f_s, f_r)):
+        for steps in (1, 2, 5, 9, 17, 33, 64, 65, 130):
+            seeds = ttga.population_seeds(2301 + steps, P)
+            s, r, g = dev(start_s), dev(start_r), dev(seeds)
+            dp.local_search(s, r, g, steps, p1, p2)
+            es, er, eg = o.local_search(start_s, start_r, seeds, steps, p1, p2)
+            assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg), steps
+    assert dp.status() == 0

@@ -33,7 +33,7 @@ constexpr int kLsCapSmall = 64;
 // Profiling build (-DTT_LS_PROF, `make libttga_prof.so`, tools/ls_prof.py):
 // per-section shader-clock totals of every wave, summed into g_ls_prof.
 #ifdef TT_LS_PROF
-enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfQ1, kPfQ1c, kPfQ1m, kPfQ2, kPfQ2c, kPfQ2m, kPfP1m2, kPfP1m2lb, kPfMaxTotal, kPfN };
+enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfQ1, kPfQ1c, kPfQ1m, kPfQ2, kPfQ2c, kPfQ2m, kPfP1m2, kPfP1m2lb, kPfP1m1m, kPfP1m1a, kPfP1m1k, kPfMaxTotal, kPfN };
 __device__ unsigned long long g_ls_prof[kPfN];
 #define LSP_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define LSP_ADD(St, i, v) ((St).prof[i] += __builtin_amdgcn_s_memtime() - (v))
@@ -882,11 +882,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                         // task 0 = t plus ei, task 1 = t_orig minus ei (kept across trials).
                         // n = corr + misc[1] + misc[0] >= corr + misc[1]: a trial that cannot
                         // win is rejected before the target slot is matched.
+#ifdef TT_LS_PROF
+                        if (!S.c1_valid) LSP_CNT(S, kPfP1m1k);
+#endif
                         if (match_tasks(S, 2)) goto redo;
                         const int lb = (fast1 ? __builtin_amdgcn_readlane(V.x, t) : corr_nb(S, ei)) + S.misc[1];
                         if (lb >= c) { S.c1_valid = 1; continue; }
+                        LSP_CNT(S, kPfP1m1m);
                         if (match_tasks(S, 1)) goto redo;
-                        if (lb + S.misc[0] < c) { accept(S); evc = 0; better = true; break; }
+                        if (lb + S.misc[0] < c) { LSP_CNT(S, kPfP1m1a); accept(S); evc = 0; better = true; break; }
                     } else {
                         if (match_tasks(S, 7)) goto redo;
                         const int n = eah_nb(S, ei) + S.misc[task_of(S, t_orig)];

@@ -1,7 +1,7 @@
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r02s; mkdir -p $O
-timeout -k 10 500 python -u tools/bench_ga.py --config comp01 --pop 65536 --children 8192 --steps 1000 --warm-gens 400 --warm-feasible 0.6 --gens 10 --cpu-sample 64 > $O/ga_p2_c8k.json 2>$O/err.log || exit $?
-cat $O/ga_p2_c8k.json
-timeout -k 10 500 python -u tools/bench_ga.py --config comp01 --pop 65536 --children 32768 --steps 1000 --warm-gens 400 --warm-feasible 0.6 --gens 5 --cpu-sample 0 > $O/ga_p2_c32k.json 2>>$O/err.log || exit $?
-cat $O/ga_p2_c32k.json
+O=gpurun_out/r02x; mkdir -p $O
+timeout -k 10 200 python -u tools/eval_variants.py med 65536 8,1032,7,1031 > $O/med.json 2>$O/err.log || exit $?
+cat $O/med.json
+timeout -k 10 200 python -u tools/eval_variants.py lg 65536 8,1032 > $O/lg.json 2>>$O/err.log || exit $?
+cat $O/lg.json

@@ -18,13 +18,18 @@ from ttga import native  # noqa: E402
 NAMES = ["init", "build_and_match", "match_task_wave", "corr_in_set", "scv_terms", "sync_accept", "feasible_now",
          "total", "trials", "event_visits", "waves", "scramble", "match_calls", "match_events", "match_steps",
          "p2_move1", "p2_move1_corr_ok", "p2_move1_match_ok", "p2_move2", "p2_move2_corr_ok", "p2_move2_match_ok",
-         "p1_move2_quick", "p1_move2_lb_ok", "max_total"]
+         "p1_move2_quick", "p1_move2_lb_ok", "p1_move1_matched", "p1_move1_accepted", "p1_move1_kept_task",
+         "max_total"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="med")
 ap.add_argument("--pop", type=int, default=4096)
 ap.add_argument("--steps", type=int, default=200)
 ap.add_argument("--pre-steps", type=int, default=0, help="untimed localSearch steps first (phase 2 start)")
+ap.add_argument("--from-ga", type=float, default=0.0,
+                help="profile the localSearch of GA children: an island (pop --pop, --children) is run until "
+                     "this fraction of it is feasible, then one generation's bred children are searched")
+ap.add_argument("--children", type=int, default=32768)
 a = ap.parse_args()
 
 lib = native.load(native.PKG_DIR / "libttga_prof.so")
@@ -36,7 +41,20 @@ dp = native.DeviceProblem(inst)
 P, E = a.pop, inst.E
 s = torch.empty((P, E), dtype=torch.uint8, device="cuda")
 r = torch.empty_like(s)
-dp.random_init(torch.from_numpy(ttga.population_seeds(1000, P)).cuda(), s, r)
+if a.from_ga > 0:
+    from ttga.ga import Island
+    isl = Island(dp, pop_size=P, children=a.children, max_steps=a.steps, seed=42)
+    isl.initialize()
+    gens = 0
+    while float(isl.pop["feasible"].float().mean().item()) < a.from_ga and gens < 400:
+        isl.step()
+        gens += 1
+    c = isl.child
+    dp.ga_breed(isl.pop["slot"], isl.pop["room"], isl.pop["penalty"], isl.rng_child, c["slot"], c["room"],
+                isl.flags, isl.p_cross, isl.p_mut, isl.skip)
+    s, r, P = c["slot"], c["room"], a.children
+else:
+    dp.random_init(torch.from_numpy(ttga.population_seeds(1000, P)).cuda(), s, r)
 if a.pre_steps:
     dp.local_search(s, r, torch.from_numpy(ttga.population_seeds(5000, P)).cuda(), a.pre_steps)
 g = torch.from_numpy(ttga.population_seeds(9000, P)).cuda()
@@ -47,7 +65,7 @@ torch.cuda.synchronize()
 n = lib.tt_ls_prof_read(buf, 1)
 v = {NAMES[i]: int(buf[i]) for i in range(n)}
 trials, waves = max(v["trials"], 1), max(v["waves"], 1)
-out = {"config": a.config, "pop": P, "max_steps": a.steps, "raw": v,
+out = {"config": a.config, "pop": P, "max_steps": a.steps, "from_ga": a.from_ga, "raw": v,
        "cycles_per_trial": {k: v[k] / trials for k in NAMES[:7]},
        "cycles_per_wave": {k: v[k] / waves for k in NAMES[:8] + ["scramble"]},
        "trials_per_wave": v["trials"] / waves, "visits_per_wave": v["event_visits"] / waves,
