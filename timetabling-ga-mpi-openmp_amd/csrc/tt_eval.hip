@@ -59,6 +59,11 @@ typedef __attribute__((address_space(4))) const int32_t ConstI32;
 
 // acc + popcount(x) as two v_bcnt_u32_b32 with accumulate (no separate add).
 // (The compiler turns the plain form into bcnt, bcnt, add3.)
+__device__ __forceinline__ int bcnt_acc(uint32_t x, int acc) {
+    int r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
 __device__ __forceinline__ int popc_acc(uint64_t x, int acc) {
     int r, t;
     asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(t) : "v"((uint32_t)x), "v"(acc));
@@ -469,7 +474,7 @@ __global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, con
 //   scv += sum_e [slot_e % 9 == 8] studentNumber[e] (:93-96)
 struct CorrLayout {
     int NWV, BST, NB, EPL;
-    size_t off_cnt, off_sl, WSI, off_acc, bytes;
+    size_t off_cnt, off_sl, WSI, off_acc, off_red, bytes;
 };
 
 __host__ __device__ inline CorrLayout corr_layout(int E, int R, int EW64, int NB) {
@@ -483,7 +488,8 @@ __host__ __device__ inline CorrLayout corr_layout(int E, int R, int EW64, int NB
     L.WSI = (L.off_sl + (size_t)E + 15) & ~(size_t)15;
     L.NB = NB;
     L.off_acc = (size_t)NB * L.WSI;
-    L.bytes = L.off_acc + (size_t)NB * 16;
+    L.off_red = L.off_acc + (size_t)NB * 16;
+    L.bytes = L.off_red + (size_t)NB * 2 * 64 * 4;
     return L;
 }
 
@@ -545,7 +551,7 @@ __device__ __forceinline__ void corr_chunk(const DevProblem& pb, int c, int lane
     }
 }
 
-template <int NB>
+template <int NB, int MEPL>
 __global__ __launch_bounds__(1024) void eval_corr_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
                                                          const uint8_t* __restrict__ room, int P,
                                                          int32_t* __restrict__ hcv_out, int32_t* __restrict__ scv_io,
@@ -558,16 +564,17 @@ __global__ __launch_bounds__(1024) void eval_corr_kernel(DevProblem pb, const ui
     const int NWV = L.NWV, pairs = (EW + 1) / 2, EPL = L.EPL;
     const uint32_t WSI = (uint32_t)L.WSI, BSTB = (uint32_t)L.BST * 8u;
     int32_t* acc = (int32_t*)(lds + L.off_acc);                  // [NB][4]: h, last, bad, -
+    int32_t* red = (int32_t*)(lds + L.off_red);                  // [NB][2][64] per-lane h, last partials
     const uint32_t lds0 = lds_addr(lds);
 
     // build-phase events of this lane and their invariants
     const int eb = (wv * 64 + lane) * EPL;
     // two events per lane from 2-byte aligned rows: one u16 load each
     const bool pair16 = EPL == 2 && (E & 1) == 0 && (((uintptr_t)slot | (uintptr_t)room) & 1) == 0;
-    uint64_t possv[kCorrMaxEPL];
-    int snv[kCorrMaxEPL];
+    uint64_t possv[MEPL];
+    int snv[MEPL];
 #pragma unroll
-    for (int j = 0; j < kCorrMaxEPL; ++j) {
+    for (int j = 0; j < MEPL; ++j) {
         const bool ok = j < EPL && eb + j < E;
         possv[j] = ok ? pb.poss[eb + j] : ~0ull;
         snv[j] = ok ? pb.sn[eb + j] : 0;
@@ -578,8 +585,8 @@ __global__ __launch_bounds__(1024) void eval_corr_kernel(DevProblem pb, const ui
         const long q0 = bt * NB;
         const int nq = (int)min((long)NB, (long)P - q0);
         __syncthreads();                                         // previous batch's outputs are read
-        for (int i = threadIdx.x; i < (int)(L.off_acc >> 4) + NB; i += blockDim.x)
-            ((uint4*)lds)[i] = make_uint4(0u, 0u, 0u, 0u);       // workspaces + acc
+        for (int i = threadIdx.x; i < (int)(L.bytes >> 4); i += blockDim.x)
+            ((uint4*)lds)[i] = make_uint4(0u, 0u, 0u, 0u);       // workspaces + acc + partials
         __syncthreads();
         // ---- build phase: the lane's events for every individual of the batch
         if (!(ablate & 1)) {
@@ -596,7 +603,7 @@ __global__ __launch_bounds__(1024) void eval_corr_kernel(DevProblem pb, const ui
                         rvq[q] = *(const uint16_t*)rrow;
                     } else {
 #pragma unroll
-                        for (int j = 0; j < kCorrMaxEPL; ++j)
+                        for (int j = 0; j < MEPL; ++j)
                             if (j < EPL && eb + j < E) {
                                 svq[q] |= (uint32_t)srow[j] << (8 * j);
                                 rvq[q] |= (uint32_t)rrow[j] << (8 * j);
@@ -614,7 +621,7 @@ __global__ __launch_bounds__(1024) void eval_corr_kernel(DevProblem pb, const ui
                 int h = 0, last = 0;
                 bool bad = false;
 #pragma unroll
-                for (int j = 0; j < kCorrMaxEPL; ++j) {
+                for (int j = 0; j < MEPL; ++j) {
                     const int e = eb + j;
                     if (j < EPL && e < E) {
                         const uint32_t s = (sv >> (8 * j)) & 0xFFu, ro = (rv >> (8 * j)) & 0xFFu;
@@ -630,14 +637,10 @@ __global__ __launch_bounds__(1024) void eval_corr_kernel(DevProblem pb, const ui
                         }
                     }
                 }
-                h = wave_sum(h);
-                last = wave_sum(last);
-                const bool anyb = __any(bad);
-                if (lane == 0) {
-                    atomicAdd(&acc[4 * q], h);
-                    atomicAdd(&acc[4 * q + 1], last);
-                    if (anyb) atomicOr(&acc[4 * q + 2], 1);
-                }
+                // per-lane partials (conflict-free, no return); summed once per batch
+                atomicAdd(&red[(2 * q) * 64 + lane], h);
+                atomicAdd(&red[(2 * q + 1) * 64 + lane], last);
+                if (__any(bad) && lane == 0) atomicOr(&acc[4 * q + 2], 1);
             }
         }
         __syncthreads();
@@ -665,10 +668,14 @@ __global__ __launch_bounds__(1024) void eval_corr_kernel(DevProblem pb, const ui
 #pragma unroll
                 for (int q = 0; q < NB; ++q) {
                     if (q >= nq) break;
-                    const int h = wave_sum(hq[q]);
-                    if (lane == 0) atomicAdd(&acc[4 * q], h);
+                    atomicAdd(&red[(2 * q) * 64 + lane], hq[q]);
                 }
             }
+        }
+        __syncthreads();
+        for (int k = wv; k < 2 * nq; k += NWV) {                 // wave-uniform: one sum per row
+            const int v = wave_sum(red[k * 64 + lane]);
+            if (lane == 0) acc[4 * (k >> 1) + (k & 1)] = v;
         }
         __syncthreads();
         if (threadIdx.x < nq) {
@@ -873,7 +880,11 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
                                feasible, penalty, ablate);
             return TT_OK;
         };
-rc = NB == 8 ? launch(eval_corr_kernel<8>) : NB == 4 ? launch(eval_corr_kernel<4>) : launch(eval_corr_kernel<2>);
+        if (CL.EPL <= 2)
+            rc = NB == 8 ? launch(eval_corr_kernel<8, 2>) : NB == 4 ? launch(eval_corr_kernel<4, 2>) : launch(eval_corr_kernel<2, 2>);
+        else
+            rc = NB == 8 ? launch(eval_corr_kernel<8, kCorrMaxEPL>)
+                 : NB == 4 ? launch(eval_corr_kernel<4, kCorrMaxEPL>) : launch(eval_corr_kernel<2, kCorrMaxEPL>);
         if (rc) return rc;
     } else if (variant == 7 || variant == 8) {
         const int NW = variant == 7 ? 4 : 8;
