@@ -31,15 +31,17 @@ struct DevProblem {
     const uint64_t* corr64;       // [E][EW64] full eventCorrelations rows (diagonal included)
     const int32_t* stc_off;       // [S+1] per-student event lists padded to multiples of 8
     const int32_t* stc_ev;        //   padding entries hold E (a sentinel column)
-    const uint4* sch;             // lane-phase records in student order: 8 u16 event ids (the
-                                  //   stc lists), bit 15 of id 0 = last record of a student
-    const int32_t* sch_part;      // record offsets of each wave's contiguous student range:
-                                  //   [kSchPart4 + w] for 4-wave, [kSchPart8 + w] for 8-wave and
-                                  //   [kSchPart16 + w] for 16-wave groups
+    const uint32_t* sid;          // lane-phase student lists, students sorted by padded size:
+                                  //   each student's events as u16 ids, padded to an even count
+                                  //   with E (the sentinel column); 64 B of slack at the end
+    const int4* srun;             // runs of equal-size students: (ids per student, first dword
+                                  //   in sid, students, 0); a wave's runs are contiguous
+    const int32_t* srun_part;     // run index range of each wave: [kSrunPart4 + w] for 4-wave,
+                                  //   [kSrunPart8 + w] for 8-wave, [kSrunPart16 + w] for 16-wave groups
     int32_t* status;              // device status word (tt_device_status)
 };
-constexpr int kSchPart4 = 0, kSchPart8 = 5, kSchPart16 = 14, kSchPartLen = 32;
-__host__ __device__ constexpr int sch_part_base(int nw) { return nw == 4 ? kSchPart4 : nw == 8 ? kSchPart8 : kSchPart16; }
+constexpr int kSrunPart4 = 0, kSrunPart8 = 5, kSrunPart16 = 14, kSrunPartLen = 32;
+__host__ __device__ constexpr int srun_part_base(int nw) { return nw == 4 ? kSrunPart4 : nw == 8 ? kSrunPart8 : kSrunPart16; }
 
 // Park-Miller "minimal standard" generator, Schrage's method
 // (Random.h:15-19, Random.cc:27-37). Bit-exact with the reference: int64

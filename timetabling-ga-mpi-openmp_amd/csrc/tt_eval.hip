@@ -124,14 +124,7 @@ __device__ __forceinline__ void corr_words(uint32_t bbase, const uint32_t* sv, c
     }
 }
 
-// ---------------------------------------------------------------- lane loop
-// Attendance masks of students whose records c0..c1-1 (8 u16 event ids each,
-// sentinel column E = slot 63, bit 15 of id 0 = the student's last record)
-// this wave owns; lane = individual, `my` = its tile row. Returns the lane's
-// >2-in-a-row + single-class count (Solution.cpp:99-137). U = 1: one record
-// per step, the next record's scalar load issued with it; U = kLanePF: four
-// records per step with the next step's records prefetched (eval_lanes; on
-// the medium instance the plain form is faster inside eval_tile5).
+// ---------------------------------------------------------------- scalar record loads
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 // 16 dwords through the scalar cache, issued now, waited for by sld_wait
 // (the compiler does not track this load: every use goes through sld_wait,
@@ -143,65 +136,119 @@ __device__ __forceinline__ u32x16 sload16(const uint32_t* p) {
 }
 __device__ __forceinline__ void sld_wait(u32x16& v) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v) : : "memory"); }
 
-constexpr int kLanePF = 4;     // lane_scv mode: 4 records per step with scalar prefetch
-
-template <int U>
-__device__ __forceinline__ int lane_scv(const uint8_t* my, const ConstU32* rec, int c0, int c1) {
+// ---------------------------------------------------------------- student runs
+// The lane phase over the size-sorted student lists (DevProblem::sid/srun):
+// a run holds `cnt` students of N ids each (N even, the last id may be the
+// sentinel E), so a student costs its own events plus at most one sentinel.
+// >2 in a row + single class of one student's attendance mask m (Solution.cpp:99-137)
+__device__ __forceinline__ int mask_scv(uint64_t m) {
+    int sc = __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);
+#pragma unroll
+    for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);
+    return sc;
+}
+// K students of N ids whose dwords are r[0 .. K*N/2)
+template <int N, int K>
+__device__ __forceinline__ int students_scv(const uint8_t* my, const u32x16& r) {
+    constexpr int H = N / 2;
+    uint32_t sl[K * N];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int j = 0; j < N; ++j) sl[k * N + j] = my[(r[k * H + (j >> 1)] >> (16 * (j & 1))) & 0xFFFFu];
     int sc = 0;
-    uint64_t m = 0;
-    auto fin = [&]() {
-        sc += __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);                          // :99-117
 #pragma unroll
-        for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);   // :119-137
-        m = 0;
-    };
-    int c = c0;
-    if constexpr (U == kLanePF) {
-        // 4 records (one s_load_dwordx16) per step, the next step's records in
-        // flight while this step's 32 ds_read_u8 run: waited for (lgkmcnt(0))
-        // at the top of the next step, so the record stream's scalar-cache
-        // misses overlap the LDS work instead of stalling every step.
-        auto step = [&](const u32x16& r) {
-            uint32_t sl[32];
+    for (int k = 0; k < K; ++k) {
+        uint64_t m = 0;
 #pragma unroll
-            for (int j = 0; j < 32; ++j) sl[j] = my[(r[j >> 1] >> (16 * (j & 1))) & 0x7FFFu];
+        for (int j = 0; j < N; ++j) m |= 1ull << (sl[k * N + j] & 63);
+        sc += mask_scv(m);
+    }
+    return sc;
+}
+// A run of cnt students of N ids from dword p: one 64-B scalar load per step
+// (two students when N <= 16), the next step's load issued before this step's
+// LDS reads (ping-pong registers).
+template <int N, int KMAX>
+__device__ __forceinline__ int run_scv(const uint8_t* my, const uint32_t* p, int cnt) {
+    constexpr int K = N <= 16 ? KMAX : 1;
+    constexpr int ST = K * N / 2;
+    const int steps = cnt / K;
+    int sc = 0;
+    if constexpr (KMAX == 1) {
+        // one student per step, its ids through the compiler's scalar loads
+        // with the next student's issued ahead (fewer SGPRs than ping-pong)
+        const ConstU32* q = (const ConstU32*)p;
+        uint32_t cur[N / 2];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+        for (int j = 0; j < N / 2; ++j) cur[j] = q[j];
+        for (int i = 0; i < cnt; ++i) {
+            const int in = i + 1 < cnt ? i + 1 : i;
+            uint32_t nxt[N / 2];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) m |= 1ull << (sl[8 * u + j] & 63);
-                if (r[4 * u] & 0x8000u) fin();
-            }
-        };
-        // ping-pong registers (no copy of a register still being loaded)
-        if (c + 4 <= c1) {
-            u32x16 ra = sload16((const uint32_t*)(rec + 4 * c)), rb;
-            while (true) {
-                sld_wait(ra);
-                rb = sload16((const uint32_t*)(rec + 4 * (c + 8 <= c1 ? c + 4 : c)));
-                step(ra);
-                c += 4;
-                if (c + 4 > c1) { sld_wait(rb); break; }
-                sld_wait(rb);
-                ra = sload16((const uint32_t*)(rec + 4 * (c + 8 <= c1 ? c + 4 : c)));
-                step(rb);
-                c += 4;
-                if (c + 4 > c1) { sld_wait(ra); break; }
-            }
+            for (int j = 0; j < N / 2; ++j) nxt[j] = q[in * (N / 2) + j];
+            uint32_t sl[N];
+#pragma unroll
+            for (int j = 0; j < N; ++j) sl[j] = my[(cur[j >> 1] >> (16 * (j & 1))) & 0xFFFFu];
+            uint64_t m = 0;
+#pragma unroll
+            for (int j = 0; j < N; ++j) m |= 1ull << (sl[j] & 63);
+            sc += mask_scv(m);
+#pragma unroll
+            for (int j = 0; j < N / 2; ++j) cur[j] = nxt[j];
+        }
+        return sc;
+    }
+    if (steps > 0) {
+        int i = 0;
+        u32x16 ra = sload16(p), rb;
+        while (true) {
+            sld_wait(ra);
+            rb = sload16(p + (i + 1 < steps ? i + 1 : i) * ST);
+            sc += students_scv<N, K>(my, ra);
+            if (++i == steps) { sld_wait(rb); break; }
+            sld_wait(rb);
+            ra = sload16(p + (i + 1 < steps ? i + 1 : i) * ST);
+            sc += students_scv<N, K>(my, rb);
+            if (++i == steps) { sld_wait(ra); break; }
         }
     }
-    if (c < c1) {
-        uint32_t cur[4] = {rec[4 * c], rec[4 * c + 1], rec[4 * c + 2], rec[4 * c + 3]};
-        for (; c < c1; ++c) {
-            const int cn = c + 1 < c1 ? c + 1 : c;
-            const uint32_t nxt[4] = {rec[4 * cn], rec[4 * cn + 1], rec[4 * cn + 2], rec[4 * cn + 3]};
-            uint32_t sl[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) sl[j] = my[(cur[j >> 1] >> (16 * (j & 1))) & 0x7FFFu];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) m |= 1ull << (sl[j] & 63);
-            if (cur[0] & 0x8000u) fin();
-#pragma unroll
-            for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+    if constexpr (K == 2) {
+        if (cnt & 1) {
+            u32x16 r = sload16(p + steps * ST);
+            sld_wait(r);
+            sc += students_scv<N, 1>(my, r);
+        }
+    }
+    return sc;
+}
+// students of more than 32 ids (no instance here has them): plain loop
+__device__ __noinline__ int run_scv_any(const uint8_t* my, const ConstU32* p, int cnt, int n) {
+    int sc = 0;
+    for (int i = 0; i < cnt; ++i) {
+        uint64_t m = 0;
+        for (int j = 0; j < n / 2; ++j) {
+            const uint32_t d = p[i * (n / 2) + j];
+            m |= 1ull << (my[d & 0xFFFFu] & 63);
+            m |= 1ull << (my[d >> 16] & 63);
+        }
+        sc += mask_scv(m);
+    }
+    return sc;
+}
+template <int KMAX>
+__device__ __forceinline__ int lane_scv_runs(const uint8_t* my, const DevProblem& pb, int r0, int r1) {
+    const ConstI32* runs = (const ConstI32*)pb.srun;
+    int sc = 0;
+    for (int k = r0; k < r1; ++k) {
+        const int n = runs[4 * k], off = runs[4 * k + 1], cnt = runs[4 * k + 2];
+        const uint32_t* p = pb.sid + off;
+        switch (n) {
+#define TT_RUN(N) case N: sc += run_scv<N, KMAX>(my, p, cnt); break;
+            TT_RUN(2) TT_RUN(4) TT_RUN(6) TT_RUN(8) TT_RUN(10) TT_RUN(12) TT_RUN(14) TT_RUN(16)
+            TT_RUN(18) TT_RUN(20) TT_RUN(22) TT_RUN(24) TT_RUN(26) TT_RUN(28) TT_RUN(30) TT_RUN(32)
+#undef TT_RUN
+            default: sc += run_scv_any(my, (const ConstU32*)p, cnt, n); break;
         }
     }
     return sc;
@@ -226,7 +273,7 @@ __host__ __device__ inline Tile5Layout tile5_layout(int E, int R, int NW) {
     return L;
 }
 
-template <int EWC, int NW, int PK, int U>
+template <int EWC, int NW, int PK>
 __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
                                                               const uint8_t* __restrict__ room, int P,
                                                               int32_t* __restrict__ hcv_out,
@@ -266,10 +313,9 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
 #pragma unroll
         for (int w = 0; w < EWC; ++w) inv_cup[r][w] = (w >= r && ok) ? pb.cupT[(size_t)w * E + e] : 0ull;
     }
-    const ConstU32* rec = (const ConstU32*)pb.sch;
-    const ConstI32* ptab = (const ConstI32*)pb.sch_part;
-    const int pbase = sch_part_base(NW);
-    const int c0 = ptab[pbase + wv], c1 = ptab[pbase + wv + 1];
+    const ConstI32* ptab = (const ConstI32*)pb.srun_part;
+    const int pbase = srun_part_base(NW);
+    const int r0 = ptab[pbase + wv], r1 = ptab[pbase + wv + 1];     // this wave's student runs
     const bool wide = (E & 15) == 0 && (((uintptr_t)slot) & 15) == 0;
     const int qpr = E >> 4;
     const uint32_t qinv = ((1u << 20) + (uint32_t)qpr - 1) / (uint32_t)max(qpr, 1);
@@ -299,7 +345,7 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
         __syncthreads();
 
         // ---- lane phase (lane = individual): attendance masks of this wave's students
-        const int sc = (!(ablate & 1) && c0 < c1) ? lane_scv<U>(tile + lane * SP, rec, c0, c1) : 0;
+        const int sc = (!(ablate & 1) && r0 < r1) ? lane_scv_runs<1>(tile + lane * SP, pb, r0, r1) : 0;
         part[wv * 64 + lane] = sc;
 
         // ---- wave phase (wave = individual): hcv terms + last-slot term
@@ -396,7 +442,7 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
 // workgroup per 64-row tile (128 KB at E = 2000: one workgroup per CU); it
 // writes the per-student scv part (>2 in a row + single class) of each
 // individual to scv_part, which eval_corr completes.
-template <int NWL, int U>
+template <int NWL>
 __global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, const uint8_t* __restrict__ slot, int P,
                                                               int32_t* __restrict__ scv_part) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -409,10 +455,9 @@ __global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, con
     uint8_t* tile = lds;
     int32_t* part = (int32_t*)(lds + (((size_t)64 * SP + 15) & ~(size_t)15));   // [NWL][64]
     const int tiles = (P + 63) / 64;
-    const ConstU32* rec = (const ConstU32*)pb.sch;
-    const ConstI32* ptab = (const ConstI32*)pb.sch_part;
-    const int pbase = sch_part_base(NWL);
-    const int c0 = ptab[pbase + wv], c1 = ptab[pbase + wv + 1];
+    const ConstI32* ptab = (const ConstI32*)pb.srun_part;
+    const int pbase = srun_part_base(NWL);
+    const int r0 = ptab[pbase + wv], r1 = ptab[pbase + wv + 1];     // this wave's student runs
     const bool wide = (E & 15) == 0 && (((uintptr_t)slot) & 15) == 0;
     const int qpr = E >> 4;
     const uint64_t qinv = ((1ull << 32) + (uint64_t)qpr - 1) / (uint64_t)max(qpr, 1);   // exact w / qpr below
@@ -439,7 +484,7 @@ __global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, con
         }
         if (threadIdx.x < 64) tile[threadIdx.x * SP + E] = 63;
         __syncthreads();
-        const int sc = c0 < c1 ? lane_scv<U>(tile + lane * SP, rec, c0, c1) : 0;
+        const int sc = r0 < r1 ? lane_scv_runs<2>(tile + lane * SP, pb, r0, r1) : 0;
         part[wv * 64 + lane] = sc;
         __syncthreads();
         if (wv == 0 && lane < np) {
@@ -865,7 +910,7 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
                 hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), lds_l, st, p->dev, slot, P, scv);
                 return TT_OK;
             };
-            rc = (ablate & 8) ? launch_l(eval_lanes_kernel<16, 1>) : launch_l(eval_lanes_kernel<16, kLanePF>);
+            rc = launch_l(eval_lanes_kernel<16>);
             if (rc) return rc;
         }
         if (ablate & 4) return check_hip(hipGetLastError(), "tt_eval launch");   // lane phase only (timing)
@@ -904,7 +949,7 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
                                feasible, penalty, ablate);
             return TT_OK;
         };
-#define TT_T5U(EWC, NWV, PKV) rc = launch(eval_tile5_kernel<EWC, NWV, PKV, 1>);
+#define TT_T5U(EWC, NWV, PKV) rc = launch(eval_tile5_kernel<EWC, NWV, PKV>);
 #define TT_T5N(EWC, NWV) \
     if (pk == 1) { TT_T5U(EWC, NWV, 1) } else if (pk == 2) { TT_T5U(EWC, NWV, 2) } else { TT_T5U(EWC, NWV, 0) }
 #define TT_T5(EWC)                                                      \

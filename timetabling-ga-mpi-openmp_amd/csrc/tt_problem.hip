@@ -115,34 +115,54 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         stc_off[s + 1] = (int32_t)stc_ev.size();
     }
     if (stc_ev.empty()) stc_ev.assign(8, E);
-    // the lane-phase records in student order: wave w of an NW-wave
-    // workgroup takes a contiguous student range, balanced by record count.
-    // sch_part[sch_part_base(NW) + w] for NW = 4, 8 and 16.
-    std::vector<uint16_t> sch;
-    std::vector<int32_t> stu_rec(S + 1, 0);
+    // Student runs for the lane phase: students sorted by their event count
+    // rounded up to even (stable), each student's ids padded with E to that
+    // count, so a student's list starts on a dword and costs its own size
+    // plus at most one sentinel (the 8-id records above pad 22 % of the ids).
+    // Wave w of an NW-wave workgroup takes a contiguous range of the sorted
+    // students balanced by ids + a per-student constant; its students form
+    // runs of one size, (size, first dword, count).
+    std::vector<uint16_t> sid;
+    std::vector<int32_t> srun_flat;                       // 4 ints per run
+    std::vector<int32_t> srun_part(kSrunPartLen, 0);
     if (E <= 32767) {
-        for (int s = 0; s < S; s++) {
-            const int c0 = stc_off[s], c1 = stc_off[s + 1];
-            for (int c = c0; c < c1; c += 8) {
-                const size_t r = sch.size();
-                for (int j = 0; j < 8; j++) sch.push_back((uint16_t)stc_ev[c + j]);
-                if (c + 8 == c1) sch[r] |= 0x8000;
+        std::vector<int> order;
+        for (int s = 0; s < S; s++)
+            if (stu_off[s + 1] > stu_off[s]) order.push_back(s);
+        auto padded = [&](int s) { const int n = stu_off[s + 1] - stu_off[s]; return n + (n & 1); };
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return padded(a) < padded(b); });
+        std::vector<int32_t> first(order.size() + 1, 0);  // dword offset of each sorted student
+        std::vector<long> cost(order.size() + 1, 0);
+        for (size_t i = 0; i < order.size(); i++) {
+            const int s = order[i];
+            first[i] = (int32_t)(sid.size() / 2);
+            for (int k = stu_off[s]; k < stu_off[s + 1]; k++) sid.push_back((uint16_t)stu_ev[k]);
+            if (sid.size() & 1) sid.push_back((uint16_t)E);
+            cost[i + 1] = cost[i] + padded(s) + 8;
+        }
+        first[order.size()] = (int32_t)(sid.size() / 2);
+        const size_t n_st = order.size();
+        for (int nw : {4, 8, 16}) {
+            const int base = srun_part_base(nw);
+            size_t i = 0;
+            for (int w = 0; w < nw; w++) {
+                srun_part[base + w] = (int32_t)(srun_flat.size() / 4);
+                const long target = cost[n_st] * (w + 1) / nw;
+                const size_t i1 = w == nw - 1 ? n_st : std::max(i, (size_t)(std::lower_bound(cost.begin(), cost.end(), target) - cost.begin()));
+                for (size_t j = i; j < i1;) {
+                    const int ne = padded(order[j]);
+                    size_t k = j;
+                    while (k < i1 && padded(order[k]) == ne) k++;
+                    srun_flat.insert(srun_flat.end(), {ne, first[j], (int32_t)(k - j), 0});
+                    j = k;
+                }
+                i = i1;
             }
-            stu_rec[s + 1] = (int32_t)(sch.size() / 8);
+            srun_part[base + nw] = (int32_t)(srun_flat.size() / 4);
         }
     }
-    std::vector<int32_t> sch_part(kSchPartLen, 0);
-    for (int nw : {4, 8, 16}) {
-        const int base = sch_part_base(nw);
-        const int total = stu_rec[S];
-        int s = 0;
-        for (int w = 0; w <= nw; w++) {
-            const long target = (long)total * w / nw;
-            while (s < S && stu_rec[s] < target) s++;
-            sch_part[base + w] = w == nw ? total : stu_rec[s];
-        }
-    }
-    if (sch.empty()) sch.assign(8, 0);
+    sid.resize(sid.size() + 32, (uint16_t)E);             // slack for 64-B scalar over-reads
+    if (srun_flat.empty()) srun_flat.assign(4, 0);
     // possibleRooms (Problem.cpp:76-95): size fits and every required feature present.
     p->poss_bits.assign(E, 0ull);
     for (int i = 0; i < E; i++)
@@ -171,8 +191,9 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         {stc_off.data(), sizeof(int32_t) * stc_off.size(), 0},
         {stc_ev.data(), sizeof(int32_t) * stc_ev.size(), 0},
         {corr64.data(), sizeof(uint64_t) * corr64.size(), 0},
-        {sch.data(), sizeof(uint16_t) * sch.size(), 0},
-        {sch_part.data(), sizeof(int32_t) * sch_part.size(), 0},
+        {sid.data(), sizeof(uint16_t) * sid.size(), 0},
+        {srun_flat.data(), sizeof(int32_t) * srun_flat.size(), 0},
+        {srun_part.data(), sizeof(int32_t) * srun_part.size(), 0},
     };
     size_t total = 0;
     for (auto& q : parts) { q.off = total; total += (q.bytes + 255) & ~(size_t)255; }
@@ -207,8 +228,9 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     d.stc_off = (const int32_t*)(base + parts[9].off);
     d.stc_ev = (const int32_t*)(base + parts[10].off);
     d.corr64 = (const uint64_t*)(base + parts[11].off);
-    d.sch = (const uint4*)(base + parts[12].off);
-    d.sch_part = (const int32_t*)(base + parts[13].off);
+    d.sid = (const uint32_t*)(base + parts[12].off);
+    d.srun = (const int4*)(base + parts[13].off);
+    d.srun_part = (const int32_t*)(base + parts[14].off);
     *out = p;
     return TT_OK;
 }

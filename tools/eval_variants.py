@@ -27,7 +27,7 @@ res = {"config": cfg, "P": P, "agree": {}, "ms_median": {}}
 for v in variants:
     # ablated (profiling-only) launches give invalid results; the wide path's
     # no-prefetch lane loop (13 | 8 << 4) does not
-    valid = {13: 8}.get(v & 15, 0)
+    valid = {}.get(v & 15, 0)
     if (v >> 4) & ~valid:
         continue
     got = dp.eval(slot, room, variant=v)
