@@ -198,7 +198,7 @@ def test_random_init_crossover_mutation_golden(problems, name):
 def test_syn_scale_instance(orc):
     """Synthetic 2000/40/10/5000 instance (BASELINE configs[4]): tt_eval takes the
     wide path; it agrees with the workgroup kernel on every individual and with
-    the oracle on a sample."""
+    the oracle (rooms and all four outputs) on 64 of them."""
     inst = ttga.config_instance("syn")
     dp = native.DeviceProblem(inst)
     assert dp.eval_variant() == 13
@@ -208,7 +208,7 @@ def test_syn_scale_instance(orc):
     hcv, scv, feas, pen = (host(t) for t in dp.eval(dev(slots), room))
     for x, y in zip((hcv, scv, feas, pen), (host(t) for t in dp.eval(dev(slots), room, variant=2))):
         assert np.array_equal(x, y)
-    idx = np.array([0, 1, 255, 511])
+    idx = np.arange(0, P, 8)                             # 64 individuals against the oracle
     o = orc.problem(inst)
     r_np = host(room)[idx]
     assert np.array_equal(o.assign_rooms(slots[idx]), r_np)
@@ -253,6 +253,30 @@ def test_local_search_random_vs_oracle(orc):
     dp.local_search(s, r, g, 3000)
     es, er, eg = o.local_search(es, er, eg, 3000)
     assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg)
+
+
+def test_local_search_med_population_vs_oracle(orc):
+    """BASELINE configs[1] at a parity size: the med instance, 96 individuals
+    from RandomInitialSolution, localSearch(200), then chained localSearch(1000)
+    and (3000) into phase 2, then eval -- every slot, room, RNG state and output
+    against the oracle (Solution.cpp:471-769)."""
+    inst = ttga.config_instance("med")
+    dp = native.DeviceProblem(inst)
+    o = orc.problem(inst)
+    P = 96
+    s0, r0, _ = o.random_init(ttga.population_seeds(4242, P))
+    seeds = ttga.population_seeds(4343, P)
+    s, r, g = dev(s0), dev(r0), dev(seeds)
+    es, er, eg = s0, r0, seeds
+    for steps in (200, 1000, 3000):
+        dp.local_search(s, r, g, steps)
+        es, er, eg = o.local_search(es, er, eg, steps)
+        assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg), steps
+    got = [host(t) for t in dp.eval(s, r)]
+    for x, e in zip(got, o.eval(es, er)):
+        assert np.array_equal(x, e)
+    assert 0 < int(got[2].sum()) < P          # both phases met (some individuals feasible, some not)
+    assert dp.status() == 0
 
 
 def test_local_search_crowded_slots_redo(orc):

@@ -108,19 +108,82 @@ __device__ __forceinline__ void lds_row_b64(uint32_t addr, uint64_t* v) {
 }
 #undef TT_RD
 
-// Correlated same-slot pairs of the lane's events (word R onwards):
-// h += popcount(cupT upper words & B[slot] words), one asm row read per event word.
+// NA consecutive 64-bit LDS words at byte address a and NB at b (NA + NB <= 8),
+// all in flight at once, waited for inside the asm.
+#define TT_O(k) [d##k] "=&v"(d[k])
+#define TT_I(k) [x##k] "v"(k < NA ? a : b), [o##k] "i"(k < NA ? 8 * k : 8 * (k - NA))
+#define TT_R(k) "ds_read_b64 %[d" #k "], %[x" #k "] offset:%[o" #k "]\n"
+template <int NA, int NB>
+__device__ __forceinline__ void lds_two_rows(uint32_t a, uint32_t b, uint64_t* v) {
+    constexpr int N = NA + NB;
+    static_assert(NA >= 1 && NB >= 0 && N <= 8, "1..8 words");
+    uint64_t d[8];
+    if constexpr (N == 8)
+        asm volatile(TT_R(0) TT_R(1) TT_R(2) TT_R(3) TT_R(4) TT_R(5) TT_R(6) TT_R(7) "s_waitcnt lgkmcnt(0)"
+                     : TT_O(0), TT_O(1), TT_O(2), TT_O(3), TT_O(4), TT_O(5), TT_O(6), TT_O(7)
+                     : TT_I(0), TT_I(1), TT_I(2), TT_I(3), TT_I(4), TT_I(5), TT_I(6), TT_I(7) : "memory");
+    else if constexpr (N == 7)
+        asm volatile(TT_R(0) TT_R(1) TT_R(2) TT_R(3) TT_R(4) TT_R(5) TT_R(6) "s_waitcnt lgkmcnt(0)"
+                     : TT_O(0), TT_O(1), TT_O(2), TT_O(3), TT_O(4), TT_O(5), TT_O(6)
+                     : TT_I(0), TT_I(1), TT_I(2), TT_I(3), TT_I(4), TT_I(5), TT_I(6) : "memory");
+    else if constexpr (N == 6)
+        asm volatile(TT_R(0) TT_R(1) TT_R(2) TT_R(3) TT_R(4) TT_R(5) "s_waitcnt lgkmcnt(0)"
+                     : TT_O(0), TT_O(1), TT_O(2), TT_O(3), TT_O(4), TT_O(5)
+                     : TT_I(0), TT_I(1), TT_I(2), TT_I(3), TT_I(4), TT_I(5) : "memory");
+    else if constexpr (N == 5)
+        asm volatile(TT_R(0) TT_R(1) TT_R(2) TT_R(3) TT_R(4) "s_waitcnt lgkmcnt(0)"
+                     : TT_O(0), TT_O(1), TT_O(2), TT_O(3), TT_O(4) : TT_I(0), TT_I(1), TT_I(2), TT_I(3), TT_I(4) : "memory");
+    else if constexpr (N == 4)
+        asm volatile(TT_R(0) TT_R(1) TT_R(2) TT_R(3) "s_waitcnt lgkmcnt(0)"
+                     : TT_O(0), TT_O(1), TT_O(2), TT_O(3) : TT_I(0), TT_I(1), TT_I(2), TT_I(3) : "memory");
+    else if constexpr (N == 3)
+        asm volatile(TT_R(0) TT_R(1) TT_R(2) "s_waitcnt lgkmcnt(0)"
+                     : TT_O(0), TT_O(1), TT_O(2) : TT_I(0), TT_I(1), TT_I(2) : "memory");
+    else if constexpr (N == 2)
+        asm volatile(TT_R(0) TT_R(1) "s_waitcnt lgkmcnt(0)" : TT_O(0), TT_O(1) : TT_I(0), TT_I(1) : "memory");
+    else
+        asm volatile(TT_R(0) "s_waitcnt lgkmcnt(0)" : TT_O(0) : TT_I(0) : "memory");
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = d[k];
+}
+#undef TT_O
+#undef TT_I
+#undef TT_R
+
+// Correlated same-slot pairs of the lane's events:
+// h += popcount(cupT upper words & B[slot] words). Event words R and EWC-1-R
+// are read together (EWC+1 row words in one asm block): ceil(EWC/2) LDS round
+// trips per individual instead of EWC.
 template <int R, int EWC>
 __device__ __forceinline__ void corr_words(uint32_t bbase, const uint32_t* sv, const uint64_t (*cup)[EWC], int lane,
                                            int E, bool last_partial, int& h) {
-    if constexpr (R < EWC) {
+#ifdef TT_NOPAIR
+    constexpr int S = R;
+#else
+    constexpr int S = EWC - 1 - R;                     // partner word
+#endif
+    if constexpr (R < S) {
+        // word S may be the last, partial one: its lanes beyond E read row 0 (harmless,
+        // their cup words are zero)
+        const uint32_t ss = (S < EWC - 1 || !last_partial || lane + 64 * S < E) ? sv[S] : 0u;
+        uint64_t bw[EWC + 1];
+        lds_two_rows<EWC - R, EWC - S>(bbase + sv[R] * (uint32_t)(EWC * 8) + 8 * R,
+                                       bbase + ss * (uint32_t)(EWC * 8) + 8 * S, bw);
+#pragma unroll
+        for (int w = R; w < EWC; ++w) h = popc_acc(cup[R][w] & bw[w - R], h);
+#pragma unroll
+        for (int w = S; w < EWC; ++w) h = popc_acc(cup[S][w] & bw[EWC - R + w - S], h);
+        corr_words<R + 1, EWC>(bbase, sv, cup, lane, E, last_partial, h);
+    } else if constexpr (R == S && R < EWC) {
         if (R < EWC - 1 || !last_partial || lane + 64 * R < E) {
             uint64_t bw[EWC - R];
             lds_row_b64<EWC - R>(bbase + sv[R] * (uint32_t)(EWC * 8) + 8 * R, bw);
 #pragma unroll
             for (int w = R; w < EWC; ++w) h = popc_acc(cup[R][w] & bw[w - R], h);
         }
+#ifdef TT_NOPAIR
         corr_words<R + 1, EWC>(bbase, sv, cup, lane, E, last_partial, h);
+#endif
     }
 }
 
