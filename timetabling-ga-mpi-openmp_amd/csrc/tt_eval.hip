@@ -157,11 +157,7 @@ __device__ __forceinline__ void lds_two_rows(uint32_t a, uint32_t b, uint64_t* v
 template <int R, int EWC>
 __device__ __forceinline__ void corr_words(uint32_t bbase, const uint32_t* sv, const uint64_t (*cup)[EWC], int lane,
                                            int E, bool last_partial, int& h) {
-#ifdef TT_NOPAIR
-    constexpr int S = R;
-#else
     constexpr int S = EWC - 1 - R;                     // partner word
-#endif
     if constexpr (R < S) {
         // word S may be the last, partial one: its lanes beyond E read row 0 (harmless,
         // their cup words are zero)
@@ -174,16 +170,13 @@ __device__ __forceinline__ void corr_words(uint32_t bbase, const uint32_t* sv, c
 #pragma unroll
         for (int w = S; w < EWC; ++w) h = popc_acc(cup[S][w] & bw[EWC - R + w - S], h);
         corr_words<R + 1, EWC>(bbase, sv, cup, lane, E, last_partial, h);
-    } else if constexpr (R == S && R < EWC) {
+    } else if constexpr (R == S) {
         if (R < EWC - 1 || !last_partial || lane + 64 * R < E) {
             uint64_t bw[EWC - R];
             lds_row_b64<EWC - R>(bbase + sv[R] * (uint32_t)(EWC * 8) + 8 * R, bw);
 #pragma unroll
             for (int w = R; w < EWC; ++w) h = popc_acc(cup[R][w] & bw[w - R], h);
         }
-#ifdef TT_NOPAIR
-        corr_words<R + 1, EWC>(bbase, sv, cup, lane, E, last_partial, h);
-#endif
     }
 }
 
