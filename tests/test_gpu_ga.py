@@ -45,7 +45,7 @@ def sm():
     return inst, native.DeviceProblem(inst), oracle().problem(inst)
 
 
-@pytest.mark.parametrize("N,C,skip", [(10, 1, 1), (10, 10, 1), (64, 37, 0), (200, 130, 1)])
+@pytest.mark.parametrize("N,C,skip", [(10, 1, 1), (10, 10, 1), (64, 37, 0), (200, 130, 1), (4096, 2048, 1)])
 def test_breed_vs_oracle(sm, N, C, skip):
     inst, dp, o = sm
     pop = oracle_population(o, N, 3 + N, 50)
@@ -60,7 +60,8 @@ def test_breed_vs_oracle(sm, N, C, skip):
     assert (fl & 1).any() and (fl & 2).any() if C >= 10 else True
 
 
-@pytest.mark.parametrize("N,C", [(10, 1), (10, 4), (300, 300), (5000, 100)])
+# N up to 65,536: the tiled sort (8,192-key LDS tiles + global steps above them)
+@pytest.mark.parametrize("N,C", [(10, 1), (10, 4), (300, 300), (5000, 100), (20000, 3000), (65536, 8192)])
 def test_replace_vs_oracle(sm, N, C):
     inst, dp, o = sm
     rng = np.random.default_rng(N + C)

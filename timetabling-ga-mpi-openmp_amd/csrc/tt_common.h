@@ -66,6 +66,25 @@ __device__ __forceinline__ double pm_next(int64_t& s) {
     return __dmul_rn(AM, (double)s);
 }
 
+// Park-Miller jump: a * b mod (2^31 - 1) for a, b < 2^31 - 1. For an in-range
+// state s (every state after the first draw), k Schrage steps give exactly
+// s * 16807^k mod (2^31 - 1).
+constexpr uint32_t kPmM = 2147483647u;
+__device__ __forceinline__ uint32_t pm_mulmod(uint32_t a, uint32_t b) {
+    const uint64_t p = (uint64_t)a * b;
+    const uint32_t r = (uint32_t)(p & kPmM) + (uint32_t)(p >> 31);
+    return r >= kPmM ? r - kPmM : r;
+}
+// 16807^(n) mod (2^31 - 1)
+__device__ __forceinline__ uint32_t pm_pow(int n) {
+    uint32_t r = 1, b = 16807u;
+    for (; n; n >>= 1) {
+        if (n & 1) r = pm_mulmod(r, b);
+        b = pm_mulmod(b, b);
+    }
+    return r;
+}
+
 // (int)(next() * n): truncation of the fp64 product (Solution.cpp:52, ga.cpp:135)
 __device__ __forceinline__ int pm_pick(int64_t& s, int n) { return (int)__dmul_rn(pm_next(s), (double)n); }
 

@@ -37,10 +37,18 @@ __global__ __launch_bounds__(64) void breed_kernel(int E, const uint8_t* __restr
     uint8_t* fl = (uint8_t*)(par + 128);             // [64]
     const long c0 = (long)blockIdx.x * 64;
     const int nc = (int)min((long)64, (long)C - c0);
+    const uint32_t skip_jump = pm_pow(3 * E - 1);
     if (lane < nc) {
         int64_t s = rng[c0 + lane];
-        if (skip_init)
-            for (int k = 0; k < 3 * E; ++k) pm_next(s);
+        if (skip_init) {
+            // the 3E discarded draws: the first one by Schrage (it brings an
+            // out-of-range seed into range), the other 3E-1 as one jump
+            pm_next(s);
+            if ((uint64_t)s < kPmM)
+                s = pm_mulmod((uint32_t)s, skip_jump);
+            else
+                for (int k = 1; k < 3 * E; ++k) pm_next(s);
+        }
         int best[2];
         for (int q = 0; q < 2; ++q) {                 // selection5 (ga.cpp:129-145)
             int b = pm_pick(s, N);
@@ -127,7 +135,35 @@ __global__ __launch_bounds__(1024) void bitonic_lds_kernel(uint64_t* __restrict_
     for (int i = threadIdx.x; i < NP; i += blockDim.x) keys[i] = sk[i];
 }
 
-// ... one global pass per (k, j) stage above that
+// ... above that, tiles of kSortTile keys in LDS: bitonic_tile_kernel runs, per
+// tile, the stages k <= kSortTile completely (full) or, for a stage k above the
+// tile, its steps j < kSortTile (after the global steps j >= kSortTile). The
+// direction of a pair is (i & k) of its global index i, as in one global pass.
+constexpr int kSortTile = 8192;
+__global__ __launch_bounds__(1024) void bitonic_tile_kernel(uint64_t* __restrict__ keys, int k_stage) {
+    __shared__ uint64_t sk[kSortTile];
+    const long base = (long)blockIdx.x * kSortTile;
+    for (int i = threadIdx.x; i < kSortTile; i += 1024) sk[i] = keys[base + i];
+    __syncthreads();
+    auto step = [&](int k, int j) {
+        for (int q = threadIdx.x; q < kSortTile / 2; q += 1024) {
+            const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1)), l = i + j;
+            const uint64_t x = sk[i], y = sk[l];
+            const bool up = ((base + i) & k) == 0;
+            if ((x > y) == up) { sk[i] = y; sk[l] = x; }
+        }
+        __syncthreads();
+    };
+    if (k_stage == 0) {
+        for (int k = 2; k <= kSortTile; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) step(k, j);
+    } else {
+        for (int j = kSortTile >> 1; j > 0; j >>= 1) step(k_stage, j);
+    }
+    for (int i = threadIdx.x; i < kSortTile; i += 1024) keys[base + i] = sk[i];
+}
+
+// one global pass of a (k, j) step with j >= kSortTile
 __global__ void bitonic_step_kernel(uint64_t* __restrict__ keys, int NP, int k, int j) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= NP) return;
@@ -260,9 +296,15 @@ extern "C" int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* po
     if (NP <= 4096) {
         hipLaunchKernelGGL(bitonic_lds_kernel, dim3(1), dim3(std::min(NP, 1024)), 0, st, keys, NP);
     } else {
-        for (int k = 2; k <= NP; k <<= 1)
-            for (int j = k >> 1; j > 0; j >>= 1)
+        // NP / kSortTile tiles: 1 + sum over the stages above the tile of (global steps + 1)
+        // launches (10 at NP = 65,536) instead of one per (k, j) step (136)
+        const int tiles = NP / kSortTile;
+        hipLaunchKernelGGL(bitonic_tile_kernel, dim3(tiles), dim3(1024), 0, st, keys, 0);
+        for (int k = 2 * kSortTile; k <= NP; k <<= 1) {
+            for (int j = k >> 1; j >= kSortTile; j >>= 1)
                 hipLaunchKernelGGL(bitonic_step_kernel, dim3((NP + 255) / 256), dim3(256), 0, st, keys, NP, k, j);
+            hipLaunchKernelGGL(bitonic_tile_kernel, dim3(tiles), dim3(1024), 0, st, keys, k);
+        }
     }
     hipLaunchKernelGGL(replace_gather_kernel, dim3(N), dim3(64), 0, st, E, N, C, keys, pop_slot, pop_room, pop_hcv,
                        pop_scv, pop_feasible, pop_penalty, child_slot, child_room, child_hcv, child_scv, child_feasible,

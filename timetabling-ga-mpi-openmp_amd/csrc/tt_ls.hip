@@ -709,21 +709,6 @@ __device__ __forceinline__ bool matchable(LsState& S, int s, int out, int a) {
 // a passing draw costs a step). The first lane that needs the full path is
 // run by the scalar code; the trials before it were rejected with their draws
 // and steps consumed, exactly as one by one.
-constexpr uint32_t kPmM = 2147483647u;
-__device__ __forceinline__ uint32_t pm_mulmod(uint32_t a, uint32_t b) {
-    const uint64_t p = (uint64_t)a * b;
-    const uint32_t r = (uint32_t)(p & kPmM) + (uint32_t)(p >> 31);
-    return r >= kPmM ? r - kPmM : r;
-}
-// 16807^(n) mod (2^31 - 1)
-__device__ __forceinline__ uint32_t pm_pow(int n) {
-    uint32_t r = 1, b = 16807u;
-    for (; n; n >>= 1) {
-        if (n & 1) r = pm_mulmod(r, b);
-        b = pm_mulmod(b, b);
-    }
-    return r;
-}
 __device__ __forceinline__ int bperm(int v, int src_lane) { return __builtin_amdgcn_ds_bpermute(src_lane << 2, v); }
 __device__ __forceinline__ uint64_t bperm64(uint64_t v, int src_lane) {
     return ((uint64_t)(uint32_t)bperm((int)(uint32_t)(v >> 32), src_lane) << 32) | (uint32_t)bperm((int)(uint32_t)v, src_lane);
