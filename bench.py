@@ -133,10 +133,16 @@ def main():
     from ttga import native
 
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; LOCAL_RANK modulo the visible GPUs and TTGA_BENCH_BACKEND=gloo
+    # let a one-GPU box rehearse the N > 1 path (RCCL needs distinct GPUs)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    backend = os.environ.get("TTGA_BENCH_BACKEND", "nccl")
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -173,7 +179,7 @@ def main():
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
 
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
@@ -202,6 +208,9 @@ def main():
                          "algorithmic_bytes": bytes_per_eval * P,
                          "kernel_ms": kernel_ms, "bytes_per_eval": bytes_per_eval},
         }
+        if world > torch.cuda.device_count():
+            line["config"]["rehearsal"] = (f"{world} ranks on {torch.cuda.device_count()} GPU(s), {backend} "
+                                           f"process group: checks the multi-rank path, not a scaling number")
         if pmc is not None:
             line["roofline"]["pipes"] = {k: pmc[k] for k in ("lds_busy", "lds_conflict", "valu_busy", "salu_busy",
                                                             "wait_any", "cycles") if k in pmc}

@@ -35,7 +35,9 @@ typedef __attribute__((address_space(4))) const uint32_t ConstU32;
 typedef __attribute__((address_space(4))) const int32_t ConstI32;
 
 // ---------------------------------------------------------------- eval_tile5
-// NW waves per 64-individual tile, persistent over tiles.
+// NW waves per 64-individual tile; one tile per workgroup (the loop also runs a
+// persistent grid). Slot rows are staged by LDS-DMA (DB: two tile buffers, the
+// next tile of a persistent grid lands under the current one's evaluation).
 //  * lane phase (LANE = INDIVIDUAL): per-student records of 8 u16 event ids
 //    (padded with the sentinel column E = slot 63, end-of-student flag in bit
 //    15) come through the scalar cache (s_load_dwordx4 via the constant
@@ -312,10 +314,12 @@ __device__ __forceinline__ int lane_scv_runs(const uint8_t* my, const DevProblem
 
 struct Tile5Layout {
     int SP, WS;
-    size_t off_ws, off_part, bytes;
+    size_t tile_bytes, off_ws, off_part, bytes;
 };
 
-__host__ __device__ inline Tile5Layout tile5_layout(int E, int R, int NW) {
+// DB: two tile buffers; the next tile's slot rows land by LDS-DMA while the
+// current one is evaluated.
+__host__ __device__ inline Tile5Layout tile5_layout(int E, int R, int NW, bool DB = false) {
     Tile5Layout L;
     int sp = (E + 1 + 3) & ~3;                 // room for the sentinel column
     if (((sp >> 2) & 1) == 0) sp += 4;         // odd dword stride: conflict-free column reads
@@ -323,13 +327,31 @@ __host__ __device__ inline Tile5Layout tile5_layout(int E, int R, int NW) {
     const int ew64 = (E + 63) / 64;
     const int cntb = ((kSlots * R + 1) / 2) * 4;
     L.WS = (kSlots * ew64 * 8 + cntb + 15) & ~15;
-    L.off_ws = ((size_t)64 * sp + 15) & ~(size_t)15;
+    L.tile_bytes = ((size_t)64 * sp + 15) & ~(size_t)15;
+    L.off_ws = (DB ? 2 : 1) * L.tile_bytes;
     L.off_part = L.off_ws + (size_t)NW * L.WS;
     L.bytes = L.off_part + 4 * (size_t)(NW * 64 + 64);
     return L;
 }
 
-template <int EWC, int NW, int PK>
+// One wave's share of a tile's slot rows by LDS-DMA (global_load_lds_dword:
+// 64 lanes x 4 B land contiguously at a wave-uniform LDS address, so a row of
+// E/4 <= 112 dwords takes two instructions and keeps its padded stride SP).
+template <int NW>
+__device__ __forceinline__ void tile_dma(const uint8_t* src, uint8_t* dst, int np, int E, int SP, int wv, int lane) {
+    const int qd = E >> 2;
+    for (int r = wv; r < np; r += NW) {
+        const uint32_t* g = (const uint32_t*)(src + (long)r * E);
+        auto* d = (__attribute__((address_space(3))) void*)(dst + r * SP);
+        if (lane < qd)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + lane), d, 4, 0, 0);
+        if (lane + 64 < qd)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + 64 + lane),
+                                             (__attribute__((address_space(3))) void*)(dst + r * SP + 256), 4, 0, 0);
+    }
+}
+
+template <int EWC, int NW, int PK, bool DB = false>
 __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
                                                               const uint8_t* __restrict__ room, int P,
                                                               int32_t* __restrict__ hcv_out,
@@ -340,7 +362,7 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
     constexpr int NT = 64 * NW;
     const int E = pb.E, R = pb.R;
     const int lane = threadIdx.x & 63, wv = wave_id();
-    const Tile5Layout L = tile5_layout(E, R, NW);
+    const Tile5Layout L = tile5_layout(E, R, NW, DB);
     const int SP = L.SP;
     uint8_t* tile = lds;
     uint8_t* ws = lds + L.off_ws + (size_t)wv * L.WS;
@@ -376,12 +398,29 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
     const int qpr = E >> 4;
     const uint32_t qinv = ((1u << 20) + (uint32_t)qpr - 1) / (uint32_t)max(qpr, 1);
 
-    for (int tl = blockIdx.x; tl < tiles; tl += gridDim.x) {
+    if constexpr (DB) {
+        // sentinel columns of both buffers (the DMA writes columns < E only), then the first tile
+        if (threadIdx.x < 128) lds[(threadIdx.x >> 6) * L.tile_bytes + (threadIdx.x & 63) * SP + E] = 63;
+        if (blockIdx.x < tiles)
+            tile_dma<NW>(slot + (long)blockIdx.x * 64 * E, lds, (int)min(64L, (long)P - (long)blockIdx.x * 64), E, SP,
+                         wv, lane);
+    }
+    int it = 0;
+    for (int tl = blockIdx.x; tl < tiles; tl += gridDim.x, ++it) {
         const long p0 = (long)tl * 64;
         const int np = (int)min((long)64, (long)P - p0);
+        const uint8_t* src = slot + p0 * E;
+        if constexpr (DB) {
+            tile = lds + (it & 1) * L.tile_bytes;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this wave's DMAs of the tile
+            __syncthreads();                                       // everyone's; the other buffer is free
+            const int tn = tl + gridDim.x;
+            if (tn < tiles)
+                tile_dma<NW>(slot + (long)tn * 64 * E, lds + ((it + 1) & 1) * L.tile_bytes,
+                             (int)min(64L, (long)P - (long)tn * 64), E, SP, wv, lane);
+        } else {
         __syncthreads();
         // ---- stage the tile's slot rows (+ sentinel column E = slot 63)
-        const uint8_t* src = slot + p0 * E;
         if (wide) {
             const uint4* s16 = (const uint4*)src;
 #pragma unroll 2
@@ -399,6 +438,7 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
         }
         if (threadIdx.x < 64) tile[threadIdx.x * SP + E] = 63;
         __syncthreads();
+        }
 
         // ---- lane phase (lane = individual): attendance masks of this wave's students
         const int sc = (!(ablate & 1) && r0 < r1) ? lane_scv_runs<1>(tile + lane * SP, pb, r0, r1) : 0;
@@ -936,10 +976,10 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
     int rc = check_pop_args(p, P, slot, room);
     if (rc) return rc;
     if (P > 0 && (!hcv || !scv || !feasible || !penalty)) { set_error("null output buffer"); return TT_ERR_INVALID; }
-    // profiling-only phase switches (results invalid): eval_tile5: 1 lane phase, 2 wave
-    // phase, 4 correlation words, 8 B-bitset atomics, 16 cell-counter atomics, 32
-    // workspace zeroing; wide path: 1 eval_corr build phase, 2 eval_corr corr phase,
-    // 4 no eval_corr launch, 8 eval_lanes without the record prefetch (valid results)
+    // profiling-only phase switches (results invalid unless noted): eval_tile5: 1 lane
+    // phase, 2 wave phase, 4 correlation words, 8 B-bitset atomics, 16 cell-counter
+    // atomics, 32 workspace zeroing, 64 persistent grid (valid results); wide path: 1
+    // eval_corr build phase, 2 eval_corr corr phase, 4 no eval_corr launch
     const int ablate = variant >> 4;
     variant &= 15;
     if (variant != 0 && variant != 2 && variant != 7 && variant != 8 && variant != 13) {
@@ -989,7 +1029,10 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
         if (rc) return rc;
     } else if (variant == 7 || variant == 8) {
         const int NW = variant == 7 ? 4 : 8;
-        const Tile5Layout TL5 = tile5_layout(E, R, NW);
+        // LDS-DMA staging into two tile buffers when rows are 4-B aligned and both
+        // buffers keep 2 workgroups per CU; else one buffer and byte copies
+        const bool db = (E & 3) == 0 && (((uintptr_t)slot) & 3) == 0 && tile5_layout(E, R, NW, true).bytes <= 80 * 1024;
+        const Tile5Layout TL5 = tile5_layout(E, R, NW, db);
         if (p->dev.EW64 > 7 || TL5.bytes > 160 * 1024 || E > 32767) {
             set_error("instance too large for the tile5 kernel");
             return TT_ERR_LIMIT;
@@ -1000,12 +1043,17 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
         auto launch = [&](auto kern) -> int {
             int per_cu = 0;
             TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, TL5.bytes));
-            const int grid = std::min(tiles, std::max(1, per_cu) * p->num_cus);
+            // one tile per workgroup: later workgroups start as earlier ones finish, so a
+            // CU's two workgroups drift out of step (one's staging under the other's
+            // compute); the persistent grid kept them in lockstep (med -3 %, lg -4 %,
+            // P = 262,144 -8 %). ablate 64: the persistent grid (comparison only).
+            const int grid = (ablate & 64) ? std::min(tiles, std::max(1, per_cu) * p->num_cus) : tiles;
             hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NW), TL5.bytes, st, p->dev, slot, room, P, hcv, scv,
                                feasible, penalty, ablate);
             return TT_OK;
         };
-#define TT_T5U(EWC, NWV, PKV) rc = launch(eval_tile5_kernel<EWC, NWV, PKV>);
+#define TT_T5U(EWC, NWV, PKV) \
+    rc = db ? launch(eval_tile5_kernel<EWC, NWV, PKV, true>) : launch(eval_tile5_kernel<EWC, NWV, PKV, false>);
 #define TT_T5N(EWC, NWV) \
     if (pk == 1) { TT_T5U(EWC, NWV, 1) } else if (pk == 2) { TT_T5U(EWC, NWV, 2) } else { TT_T5U(EWC, NWV, 0) }
 #define TT_T5(EWC)                                                      \
