@@ -119,6 +119,13 @@ int tt_mutation(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng,
 int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P, int max_steps,
                     double p1, double p2, double p3, void* stream);
 
+/* tt_local_search with the individuals dispatched in the order order[0..P-1]
+ * (device i32, a permutation of 0..P-1; NULL: 0..P-1). Every individual's
+ * result is the same as tt_local_search's; only the wave launch order changes
+ * (longest-expected first shortens the launch's tail). */
+int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P, int max_steps,
+                            double p1, double p2, double p3, const int32_t* order, void* stream);
+
 /* ---- GA generation primitives (ga.cpp:510-588, batched over C children) ----
  * Population (caller-owned, device): pop_slot/pop_room [N][E], pop_hcv,
  * pop_scv, pop_penalty i32[N], pop_feasible u8[N]; kept sorted by penalty.

@@ -79,11 +79,11 @@ def test_replace_vs_oracle(sm, N, C):
         assert np.array_equal(host(gpop[k]), exp[k]), k
 
 
-@pytest.mark.parametrize("N,C,gens", [(10, 1, 12), (16, 8, 6)])
-def test_island_generations_vs_oracle(sm, N, C, gens):
+@pytest.mark.parametrize("N,C,gens,lpt", [(10, 1, 12, None), (16, 8, 6, None), (64, 48, 4, True)])
+def test_island_generations_vs_oracle(sm, N, C, gens, lpt):
     inst, dp, o = sm
     steps, seed = 120, 29
-    isl = Island(dp, pop_size=N, children=C, max_steps=steps, seed=seed)
+    isl = Island(dp, pop_size=N, children=C, max_steps=steps, seed=seed, lpt=lpt)
     isl.initialize()
     for _ in range(gens):
         isl.step()

@@ -279,6 +279,24 @@ def test_local_search_med_population_vs_oracle(orc):
     assert dp.status() == 0
 
 
+def test_local_search_ordered_dispatch():
+    """tt_local_search_ordered: any dispatch order gives tt_local_search's
+    results (slots, rooms, RNG states), on the small-task + redo path too."""
+    for name, P in (("med", 150), ("sm", 70)):
+        inst = ttga.config_instance(name)
+        dp = native.DeviceProblem(inst)
+        seeds = ttga.population_seeds(515, P)
+        s0 = dev(ttga.random_slots(seeds, inst.E)[0])
+        r0 = dp.assign_rooms(s0)
+        runs = []
+        for order in (None, torch.randperm(P, generator=torch.Generator().manual_seed(3)).int().cuda()):
+            s, r, g = s0.clone(), r0.clone(), dev(ttga.population_seeds(616, P))
+            dp.local_search(s, r, g, 400, order=order)
+            runs.append((host(s), host(r), host(g)))
+        for a, b in zip(*runs):
+            assert np.array_equal(a, b), name
+
+
 def test_local_search_crowded_slots_redo(orc):
     """tt_local_search runs a first launch whose matcher tasks hold 64 events per
     slot; an individual whose trial touches a slot with more events is redone

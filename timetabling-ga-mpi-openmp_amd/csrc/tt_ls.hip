@@ -748,11 +748,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
                                                           uint8_t* __restrict__ room, int64_t* __restrict__ rng,
                                                           int P, int max_steps, double p1, double p2, double p3,
                                                           uint8_t* __restrict__ redo_out,
-                                                          const uint8_t* __restrict__ redo_in) {
+                                                          const uint8_t* __restrict__ redo_in,
+                                                          const int32_t* __restrict__ order) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int E = pb.E, R = pb.R, EW = pb.EW64;
     const int lane = threadIdx.x;
-    const long p = blockIdx.x;
+    const long p = order ? (long)order[blockIdx.x] : (long)blockIdx.x;   // dispatch order only
     if (redo_in && !redo_in[p]) return;
     LSP_T(t_kernel);
     const LsLayout L = ls_layout(E, R, EW, CAP);
@@ -1198,6 +1199,12 @@ extern "C" int tt_ls_prof_read(unsigned long long* out, int reset) {
 
 extern "C" int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P,
                                int max_steps, double p1, double p2, double p3, void* stream) {
+    return tt_local_search_ordered(p, slot, room, rng, P, max_steps, p1, p2, p3, nullptr, stream);
+}
+
+extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P,
+                                       int max_steps, double p1, double p2, double p3, const int32_t* order,
+                                       void* stream) {
     int rc = check_pop_args(p, P, slot, room);
     if (rc || P == 0) return rc;
     if (!rng) { set_error("null rng buffer"); return TT_ERR_INVALID; }
@@ -1208,7 +1215,7 @@ extern "C" int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room
     hipStream_t st = (hipStream_t)stream;
     if (p->E <= kLsCapSmall) {                      // no slot can exceed the small tasks
         hipLaunchKernelGGL(local_search_kernel<kMaxSlotEvents>, dim3(P), dim3(64), Lf.bytes, st, p->dev, slot, room,
-                           rng, P, max_steps, p1, p2, p3, (uint8_t*)nullptr, (const uint8_t*)nullptr);
+                           rng, P, max_steps, p1, p2, p3, (uint8_t*)nullptr, (const uint8_t*)nullptr, order);
         return check_hip(hipGetLastError(), "local_search launch");
     }
     const LsLayout Ls = ls_layout(p->E, p->R, p->dev.EW64, kLsCapSmall);
@@ -1216,10 +1223,10 @@ extern "C" int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room
     TT_HIP(hipMallocAsync((void**)&redo, (size_t)P, st));
     TT_HIP(hipMemsetAsync(redo, 0, (size_t)P, st));
     hipLaunchKernelGGL(local_search_kernel<kLsCapSmall>, dim3(P), dim3(64), Ls.bytes, st, p->dev, slot, room, rng, P,
-                       max_steps, p1, p2, p3, redo, (const uint8_t*)nullptr);
+                       max_steps, p1, p2, p3, redo, (const uint8_t*)nullptr, order);
     TT_HIP(hipGetLastError());
     hipLaunchKernelGGL(local_search_kernel<kMaxSlotEvents>, dim3(P), dim3(64), Lf.bytes, st, p->dev, slot, room, rng,
-                       P, max_steps, p1, p2, p3, (uint8_t*)nullptr, (const uint8_t*)redo);
+                       P, max_steps, p1, p2, p3, (uint8_t*)nullptr, (const uint8_t*)redo, order);
     TT_HIP(hipGetLastError());
     TT_HIP(hipFreeAsync(redo, st));
     return TT_OK;

@@ -141,7 +141,7 @@ class Island(Members):
 
     def __init__(self, dp, pop_size: int = 10, children: int = 1, max_steps: int = 200, seed: int = 1,
                  p_cross: float = 0.8, p_mut: float = 0.5, skip_init_draws: bool = True, device=None,
-                 p1: float = 1.0, p2: float = 1.0, p3: float = 0.0):
+                 p1: float = 1.0, p2: float = 1.0, p3: float = 0.0, lpt: bool | None = None):
         import torch
         if not (1 <= children <= pop_size):
             raise ValueError("need 1 <= children <= pop_size")
@@ -151,6 +151,9 @@ class Island(Members):
         self.max_steps, self.seed = int(max_steps), int(seed)
         self.p_cross, self.p_mut, self.skip = float(p_cross), float(p_mut), bool(skip_init_draws)
         self.p1, self.p2, self.p3 = float(p1), float(p2), float(p3)   # LS move probabilities (Solution.h:61)
+        # longest-expected-first dispatch of the children's local search (only the
+        # launch order changes); by default for generations of >= 4096 children
+        self.lpt = (int(children) >= 4096) if lpt is None else bool(lpt)
         self.child = new_population(self.C, dp.E, dev)
         self.flags = torch.zeros(self.C, dtype=torch.uint8, device=dev)
         self.rng_init = torch.from_numpy(stream_seeds(seed, 0, self.N)).to(dev)
@@ -171,10 +174,18 @@ class Island(Members):
 
     def step(self):
         """One generation of C children (ga.cpp:543-585)."""
+        import torch
         c = self.child
         self.dp.ga_breed(self.pop["slot"], self.pop["room"], self.pop["penalty"], self.rng_child, c["slot"], c["room"],
                          self.flags, self.p_cross, self.p_mut, self.skip)
-        self.dp.local_search(c["slot"], c["room"], self.rng_child, self.max_steps, self.p1, self.p2, self.p3)
+        order = None
+        if self.lpt:
+            # dispatch the children longest-expected first (hcv before the search,
+            # descending): the launch's tail is its slowest waves; results unchanged
+            self._evaluate(c)
+            order = torch.argsort(c["hcv"], descending=True, stable=True).to(torch.int32)
+        self.dp.local_search(c["slot"], c["room"], self.rng_child, self.max_steps, self.p1, self.p2, self.p3,
+                             order=order)
         self._evaluate(c)
         self.dp.ga_replace(self.pop, c, self.work)
         self.generation += 1

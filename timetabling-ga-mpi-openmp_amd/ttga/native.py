@@ -23,7 +23,7 @@ EXPORTS = (
     "tt_problem_create", "tt_problem_destroy", "tt_problem_dims", "tt_problem_derived", "tt_eval",
     "tt_eval_variant", "tt_assign_rooms", "tt_random_init", "tt_crossover", "tt_mutation", "tt_local_search",
     "tt_device_status", "tt_last_error", "tt_version", "tt_ga_breed", "tt_ga_work_bytes", "tt_ga_replace",
-    "tt_eval_auto_variant",
+    "tt_eval_auto_variant", "tt_local_search_ordered",
 )
 
 _lib = None
@@ -57,6 +57,7 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.tt_crossover.argtypes = [vp, vp, vp, vp, vp, vp, i32, vp]
     lib.tt_mutation.argtypes = [vp, vp, vp, vp, i32, vp]
     lib.tt_local_search.argtypes = [vp, vp, vp, vp, i32, i32, dbl, dbl, dbl, vp]
+    lib.tt_local_search_ordered.argtypes = [vp, vp, vp, vp, i32, i32, dbl, dbl, dbl, vp, vp]
     lib.tt_device_status.argtypes = [vp, vp]
     lib.tt_eval_auto_variant.argtypes = [vp]
     lib.tt_ga_breed.argtypes = [vp, vp, vp, vp, i32, vp, i32, dbl, dbl, i32, vp, vp, vp, vp]
@@ -184,12 +185,22 @@ class DeviceProblem:
         _check(self.lib, self.lib.tt_mutation(self.handle, slot.data_ptr(), room.data_ptr(), rng.data_ptr(), P,
                                               self._stream(slot)))
 
-    def local_search(self, slot, room, rng, max_steps: int, p1=1.0, p2=1.0, p3=0.0):
+    def local_search(self, slot, room, rng, max_steps: int, p1=1.0, p2=1.0, p3=0.0, order=None):
+        """order: optional int32 device permutation, the dispatch order (results unchanged)."""
+        import torch
         P = self._pop(slot, room)
         self._rng(rng, P)
-        _check(self.lib, self.lib.tt_local_search(self.handle, slot.data_ptr(), room.data_ptr(), rng.data_ptr(), P,
-                                                  int(max_steps), float(p1), float(p2), float(p3),
-                                                  self._stream(slot)))
+        if order is None:
+            _check(self.lib, self.lib.tt_local_search(self.handle, slot.data_ptr(), room.data_ptr(), rng.data_ptr(),
+                                                      P, int(max_steps), float(p1), float(p2), float(p3),
+                                                      self._stream(slot)))
+            return
+        if not (order.is_cuda and order.dtype == torch.int32 and order.is_contiguous() and order.numel() == P):
+            raise ValueError("order must be a contiguous int32 CUDA tensor of P entries")
+        _check(self.lib, self.lib.tt_local_search_ordered(self.handle, slot.data_ptr(), room.data_ptr(),
+                                                          rng.data_ptr(), P, int(max_steps), float(p1), float(p2),
+                                                          float(p3), ctypes.c_void_p(order.data_ptr()),
+                                                          self._stream(slot)))
 
     # -- GA generation primitives ---------------------------------------------------
     def ga_breed(self, pop_slot, pop_room, pop_penalty, rng, child_slot, child_room, child_flags,

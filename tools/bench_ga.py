@@ -54,11 +54,14 @@ ap.add_argument("--seed", type=int, default=42)
 ap.add_argument("--cpu-sample", type=int, default=512)
 ap.add_argument("--warm-gens", type=int, default=0, help="at most this many untimed generations first")
 ap.add_argument("--warm-feasible", type=float, default=1.1, help="stop warming once this fraction is feasible")
+ap.add_argument("--lpt", choices=["auto", "on", "off"], default="auto",
+                help="longest-expected-first dispatch of the children's local search (Island default: auto)")
 a = ap.parse_args()
 
 inst = ttga.config_instance(a.config)
 dp = native.DeviceProblem(inst)
-isl = Island(dp, pop_size=a.pop, children=a.children, max_steps=a.steps, seed=a.seed)
+isl = Island(dp, pop_size=a.pop, children=a.children, max_steps=a.steps, seed=a.seed,
+             lpt=None if a.lpt == "auto" else a.lpt == "on")
 torch.cuda.synchronize()
 t0 = time.perf_counter()
 isl.initialize()
@@ -82,7 +85,8 @@ torch.cuda.synchronize()
 gpu_s = time.perf_counter() - t0
 feas, scv, hcv, pen = isl.member_meta(0)
 out = {"config": a.config, "E": inst.E, "R": inst.R, "F": inst.F, "S": inst.S, "pop": a.pop,
-       "children_per_gen": a.children, "gens": a.gens, "max_steps": a.steps, "init_seconds": init_s,
+       "children_per_gen": a.children, "gens": a.gens, "max_steps": a.steps, "lpt_dispatch": isl.lpt,
+       "init_seconds": init_s,
        "warm_gens": warm, "feasible_fraction_at_start": feas_start,
        "gpu_seconds": gpu_s, "gpu_children_per_s": a.children * a.gens / gpu_s,
        "best": {"feasible": feas, "scv": scv, "hcv": hcv, "penalty": pen},
