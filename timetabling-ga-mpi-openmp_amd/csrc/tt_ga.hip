@@ -20,81 +20,77 @@ namespace ttga {
 constexpr uint8_t kFlagCross = 1, kFlagMutate = 2;
 
 // ---------------------------------------------------------------- breed
-// Lane per child for the RNG-sequential part (selection, the E crossover
-// draws recorded as a bitmask in LDS, the mutation draw); then the wave builds
-// each child row with coalesced reads of its parents' rows.
-__global__ __launch_bounds__(64) void breed_kernel(int E, const uint8_t* __restrict__ pop_slot,
-                                                   const uint8_t* __restrict__ pop_room,
-                                                   const int32_t* __restrict__ pen, int N,
-                                                   int64_t* __restrict__ rng, int C, double p_cross, double p_mut,
-                                                   int skip_init, uint8_t* __restrict__ child_slot,
-                                                   uint8_t* __restrict__ child_room, uint8_t* __restrict__ flags) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int lane = threadIdx.x;
-    const int EW = (E + 63) / 64;
-    uint64_t* pick = (uint64_t*)lds;                 // [64][EW] bit e set: take parent a's slot
-    int32_t* par = (int32_t*)(pick + 64 * EW);       // [64][2]
-    uint8_t* fl = (uint8_t*)(par + 128);             // [64]
-    const long c0 = (long)blockIdx.x * 64;
-    const int nc = (int)min((long)64, (long)C - c0);
-    const uint32_t skip_jump = pm_pow(3 * E - 1);
-    if (lane < nc) {
-        int64_t s = rng[c0 + lane];
-        if (skip_init) {
-            // the 3E discarded draws: the first one by Schrage (it brings an
-            // out-of-range seed into range), the other 3E-1 as one jump
-            pm_next(s);
-            if ((uint64_t)s < kPmM)
-                s = pm_mulmod((uint32_t)s, skip_jump);
-            else
-                for (int k = 1; k < 3 * E; ++k) pm_next(s);
-        }
-        int best[2];
-        for (int q = 0; q < 2; ++q) {                 // selection5 (ga.cpp:129-145)
-            int b = pm_pick(s, N);
-            for (int i = 1; i < 5; ++i) {
-                const int t = pm_pick(s, N);
-                if ((uint32_t)pen[t] < (uint32_t)pen[b]) b = t;   // an invalid genome (-1) never wins
-            }
-            best[q] = b;
-        }
-        uint8_t f = 0;
-        uint64_t* pk = pick + lane * EW;
-        if (pm_next(s) < p_cross) {                   // crossover (Solution.cpp:896-903)
-            f |= kFlagCross;
-            for (int w = 0; w < EW; ++w) {
-                uint64_t m = 0;
-                const int n = min(64, E - 64 * w);
-                for (int b = 0; b < n; ++b)
-                    if (pm_next(s) < 0.5) m |= 1ull << b;
-                pk[w] = m;
-            }
-        }
-        if (pm_next(s) < p_mut) f |= kFlagMutate;
-        rng[c0 + lane] = s;
-        par[2 * lane] = best[0];
-        par[2 * lane + 1] = best[1];
-        fl[lane] = f;
+// One wave per child. Every lane replays the child's short sequential draws
+// (the 3E discarded draws as one Park-Miller jump, the ten selection5 picks,
+// the crossover and mutation draws); the E crossover picks, one per event,
+// are drawn 64 at a time: event e = 64b + l takes state * 16807^(e+1), i.e.
+// lane l multiplies its 16807^(l+1) by 16807^(64b) -- the same states the
+// sequential loop would produce (Random.cc:27-37 for in-range states). The
+// wave then writes its child row with coalesced byte stores.
+__global__ __launch_bounds__(256) void breed_kernel(int E, const uint8_t* __restrict__ pop_slot,
+                                                    const uint8_t* __restrict__ pop_room,
+                                                    const int32_t* __restrict__ pen, int N,
+                                                    int64_t* __restrict__ rng, int C, double p_cross, double p_mut,
+                                                    int skip_init, uint32_t jump_skip, uint32_t jump_e,
+                                                    uint8_t* __restrict__ child_slot, uint8_t* __restrict__ child_room,
+                                                    uint8_t* __restrict__ flags) {
+    const int lane = threadIdx.x & 63;
+    const long ch = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (ch >= C) return;                              // wave-uniform
+    int64_t s = rng[ch];
+    if (skip_init) {
+        // the 3E discarded draws (ga.cpp:543-548): the first by Schrage (it brings an
+        // out-of-range seed into range), the other 3E-1 as one jump
+        pm_next(s);
+        if ((uint64_t)s < kPmM)
+            s = pm_mulmod((uint32_t)s, jump_skip);
+        else
+            for (int k = 1; k < 3 * E; ++k) pm_next(s);
     }
-    __syncthreads();
-    for (int c = 0; c < nc; ++c) {
-        const long ch = c0 + c;
-        const int a = par[2 * c], b = par[2 * c + 1];
-        const uint8_t f = fl[c];
-        const uint8_t* sa = pop_slot + (long)a * E;
-        const uint8_t* sb = pop_slot + (long)b * E;
-        const uint8_t* ra = pop_room + (long)a * E;
-        const uint64_t* pk = pick + c * EW;
-        for (int e = lane; e < E; e += 64) {
-            if (f & kFlagCross) {
-                child_slot[ch * E + e] = ((pk[e >> 6] >> (e & 63)) & 1ull) ? sa[e] : sb[e];
-            } else {
-                child_slot[ch * E + e] = sa[e];
-                child_room[ch * E + e] = ra[e];
-            }
+    int best[2];
+    for (int q = 0; q < 2; ++q) {                     // selection5 (ga.cpp:129-145)
+        int b = pm_pick(s, N);
+        for (int i = 1; i < 5; ++i) {
+            const int t = pm_pick(s, N);
+            if ((uint32_t)pen[t] < (uint32_t)pen[b]) b = t;   // an invalid genome (-1) never wins
         }
-        if (lane == 0) flags[ch] = f;
+        best[q] = b;
     }
+    const uint8_t* sa = pop_slot + (long)best[0] * E;
+    const uint8_t* sb = pop_slot + (long)best[1] * E;
+    uint8_t* cs = child_slot + ch * E;
+    uint8_t f = 0;
+    if (pm_next(s) < p_cross) {                       // crossover (Solution.cpp:896-903)
+        f |= kFlagCross;
+        const uint32_t base = (uint32_t)s;            // in range: ten draws were taken
+        const uint32_t a64 = pm_pow(64);
+        uint32_t cur = pm_mulmod(base, pm_pow(lane + 1));
+        for (int e = lane; e - lane < E; e += 64) {   // wave-uniform trip count
+            const bool take_a = __dmul_rn(1.0 / 2147483647.0, (double)cur) < 0.5;
+            if (e < E) cs[e] = take_a ? sa[e] : sb[e];
+            cur = pm_mulmod(cur, a64);
+        }
+        s = pm_mulmod(base, jump_e);                  // the state after the E picks
+    } else {
+        const uint8_t* ra = pop_room + (long)best[0] * E;
+        uint8_t* cr = child_room + ch * E;
+        for (int e = lane; e < E; e += 64) { cs[e] = sa[e]; cr[e] = ra[e]; }
+    }
+    if (pm_next(s) < p_mut) f |= kFlagMutate;
+    if (lane == 0) {
+        rng[ch] = s;
+        flags[ch] = f;
+    }
+}
+
+// 16807^n mod (2^31 - 1) on the host (the breed jumps)
+static uint32_t host_pm_pow(long n) {
+    uint64_t r = 1, b = 16807;
+    for (; n > 0; n >>= 1) {
+        if (n & 1) r = r * b % 2147483647ull;
+        b = b * b % 2147483647ull;
+    }
+    return (uint32_t)r;
 }
 
 // ---------------------------------------------------------------- replace + sort
@@ -256,10 +252,9 @@ extern "C" int tt_ga_breed(const tt_problem* p, const uint8_t* pop_slot, const u
     if (C == 0) return TT_OK;
     if ((rc = use_device(p))) return rc;
     hipStream_t st = (hipStream_t)stream;
-    const int EW = (p->E + 63) / 64;
-    const size_t lds = 8 * (size_t)64 * EW + 4 * 128 + 64;
-    hipLaunchKernelGGL(breed_kernel, dim3((C + 63) / 64), dim3(64), lds, st, p->E, pop_slot, pop_room, pop_penalty, N,
-                       rng, C, p_cross, p_mut, skip_init_draws, child_slot, child_room, child_flags);
+    const uint32_t jump_skip = host_pm_pow(3L * p->E - 1), jump_e = host_pm_pow(p->E);
+    hipLaunchKernelGGL(breed_kernel, dim3((C + 3) / 4), dim3(256), 0, st, p->E, pop_slot, pop_room, pop_penalty, N,
+                       rng, C, p_cross, p_mut, skip_init_draws, jump_skip, jump_e, child_slot, child_room, child_flags);
     if ((rc = check_hip(hipGetLastError(), "breed launch"))) return rc;
     if ((rc = launch_assign_masked(p, child_slot, child_room, C, child_flags, kFlagCross, st))) return rc;
     return launch_mutation_masked(p, child_slot, child_room, rng, C, child_flags, kFlagMutate, st);
