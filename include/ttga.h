@@ -73,24 +73,21 @@ int tt_eval(const tt_problem* p, const uint8_t* slot, const uint8_t* room, int P
             uint8_t* feasible, int32_t* penalty, void* stream);
 
 /* tt_eval with an explicit kernel choice, for tests and profiling:
- *   0 = automatic (8 when E <= 448, else 13 when it fits, else 1 or 2),
- *   1 = eval_tile, 8-wave tile of 64 individuals (E <= 1024),
+ *   0 = automatic (8 when its LDS fits, else 7, else 13, else 2),
  *   2 = eval_block, one workgroup per individual (any E),
- *   3 = eval_tile4, 4-wave tile, 4 workgroups per CU (E <= 448),
- *   4 = eval_tile4 with 8 waves (E <= 448),
- *   5/6 = eval_tile5, 4/8 waves, wave workspaces on top of the tile, u32 cell
- *         counters (E <= 448),
- *   7/8 = eval_tile5, 4/8 waves, tile kept, packed u16 cell counters (E <= 448),
- *   9/10 = the two phases of eval_tile5 as two launches (8/4-wave lane phase),
- *   13 = wide path: 16-wave lane-phase tile + wave-per-individual hcv with
- *        streamed correlation words (E <= 2490, the 64-row tile must fit
- *        the LDS; automatic for E > 448).
- * All variants give identical results. */
+ *   7/8 = eval_tile5, 4/8 waves per 64-individual tile (E <= 448): a
+ *         lane-per-individual phase (attendance masks) and a wave-per-individual
+ *         phase (bitset hard constraints), slot rows staged by LDS-DMA,
+ *   13 = wide path: eval_lanes (16-wave lane-phase tile) + eval_corr (batches
+ *        of individuals against the streamed correlation triangle; E <= 2490,
+ *        the 64-row tile must fit the LDS; automatic for E > 448).
+ * Bits 4 and up of `variant` are profiling switches (csrc/tt_eval.hip); most
+ * of them give invalid results. All variants give identical results. */
 int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const uint8_t* room, int P, int32_t* hcv,
                     int32_t* scv, uint8_t* feasible, int32_t* penalty, int variant, void* stream);
 
-/* The variant tt_eval chooses for this instance: 8 (E <= 448), 13 (the wide
- * path, E <= 2490), else 2 (eval_block); -1 for a null handle. */
+/* The variant tt_eval chooses for this instance: 8 or 7 (E <= 448), 13 (the
+ * wide path, E <= 2490), else 2 (eval_block); -1 for a null handle. */
 int tt_eval_auto_variant(const tt_problem* p);
 
 /* Solution::assignRooms (Solution.cpp:772-891) on every non-empty timeslot in
