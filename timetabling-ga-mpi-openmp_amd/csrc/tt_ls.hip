@@ -754,6 +754,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void lo
     const int E = pb.E, R = pb.R, EW = pb.EW64;
     const int lane = threadIdx.x;
     const long p = order ? (long)order[blockIdx.x] : (long)blockIdx.x;   // dispatch order only
+    if ((unsigned long)p >= (unsigned long)P) return;                     // not a permutation entry
     if (redo_in && !redo_in[p]) return;
     LSP_T(t_kernel);
     const LsLayout L = ls_layout(E, R, EW, CAP);
