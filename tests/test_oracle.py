@@ -145,3 +145,24 @@ def test_oracle_vs_reference_random(orc, seed):
     seeds = ttga.population_seeds(seed * 77, 6)
     for a, b in zip(ho.local_search(slots[:6], ro[:6], seeds, 300), hr.local_search(slots[:6], rr[:6], seeds, 300)):
         assert np.array_equal(a, b)
+
+
+@needs_ref
+def test_oracle_vs_reference_med_ls_chain(orc):
+    """The chain of tests/test_gpu_parity.py::test_local_search_med_population_vs_oracle
+    (med, 96 individuals, localSearch 200 -> 1000 -> 3000 into phase 2), run by the
+    reference's own Solution code: the oracle that checks the GPU there equals it
+    here, so the GPU result is pinned to the reference on that population."""
+    inst = ttga.config_instance("med")
+    ho, hr = orc.problem(inst), REF.problem(inst)
+    P = 96
+    s0, r0, _ = ho.random_init(ttga.population_seeds(4242, P))
+    seeds = ttga.population_seeds(4343, P)
+    a, b = (s0, r0, seeds), (s0, r0, seeds)
+    for steps in (200, 1000, 3000):
+        a = ho.local_search(*a, steps)
+        b = hr.local_search(*b, steps)
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y), steps
+    for x, y in zip(ho.eval(a[0], a[1]), hr.eval(b[0], b[1])):
+        assert np.array_equal(x, y)
