@@ -123,6 +123,13 @@ int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* 
 int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P, int max_steps,
                             double p1, double p2, double p3, const int32_t* order, void* stream);
 
+/* A longest-expected-first dispatch order for tt_local_search_ordered:
+ * order[0..n-1] = the indices of key[0..n-1] (device i32, e.g. the children's
+ * hcv before their local search) by key descending, ties by index, negative
+ * keys last. work: device scratch of at least 8 * (n rounded up to a power of
+ * two) bytes (tt_ga_work_bytes(n, E) suffices). */
+int tt_lpt_order(const tt_problem* p, const int32_t* key, int n, int32_t* order, void* work, void* stream);
+
 /* ---- GA generation primitives (ga.cpp:510-588, batched over C children) ----
  * Population (caller-owned, device): pop_slot/pop_room [N][E], pop_hcv,
  * pop_scv, pop_penalty i32[N], pop_feasible u8[N]; kept sorted by penalty.

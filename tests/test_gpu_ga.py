@@ -170,6 +170,37 @@ def test_native_driver_matches_python_driver(tmp_path, sm):
     assert_validated(inst, tim, cc.stdout)
 
 
+def test_lpt_order_vs_numpy(sm):
+    """tt_lpt_order: indices by key descending, ties by index, negative keys last
+    (the sizes cover the one-workgroup sort and the tiled one)."""
+    inst, dp, o = sm
+    rng = np.random.default_rng(8)
+    for n in (1, 100, 4096, 5000, 20000):
+        key = rng.integers(-1, 30, n).astype(np.int32)
+        hi = np.where(key < 0, np.int64(2 ** 32), np.int64(2 ** 31 - 1) - key.astype(np.int64))
+        exp = np.lexsort((np.arange(n), hi)).astype(np.int32)
+        got = host(dp.lpt_order(dev(key), dp.ga_work(max(n, 2))))
+        assert np.array_equal(got, exp), n
+
+
+def test_native_driver_matches_python_driver_lpt(tmp_path, sm):
+    """Both drivers with 4,096 children per generation (longest-expected-first
+    dispatch in both): identical JSON lines apart from wall-clock times."""
+    inst, dp, o = sm
+    exe = REPO / "timetabling-ga-mpi-openmp_amd" / "ttga-ga"
+    tim = tmp_path / "sm.tim"
+    ttga.write_tim(inst, tim)
+    args = ["-i", str(tim), "-s", "5", "-p", "1", "-c", "4096", "--generations", "6", "--pop", "4096"]
+    env = dict(__import__("os").environ, PYTHONPATH=str(REPO / "timetabling-ga-mpi-openmp_amd"))
+    py = subprocess.run([sys.executable, "-m", "ttga.islands", *args], capture_output=True, text=True, timeout=240,
+                        env=env, cwd=str(tmp_path))
+    cc = subprocess.run([str(exe), *args], capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    assert py.returncode == 0, py.stderr[-2000:]
+    assert cc.returncode == 0, cc.stderr[-2000:]
+    a, b = _json_lines(py.stdout), _json_lines(cc.stdout)
+    assert len(a) >= 3 and a == b
+
+
 def test_ga_trajectories_match_reference_statistically(sm):
     """Whole-GA outcomes over fixed seeds (the RNG streams differ):
     the device GA (pop 10, one child per generation) against the reference's

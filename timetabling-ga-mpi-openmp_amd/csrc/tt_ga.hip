@@ -219,6 +219,22 @@ __global__ __launch_bounds__(64) void replace_scatter_kernel(int E, const uint8_
     }
 }
 
+// keys for a longest-expected-first order: larger key first, ties by index,
+// negative keys (invalid genomes) last; padding keys sort after all
+__global__ void lpt_keys_kernel(const int32_t* __restrict__ key, int n, int NP, uint64_t* __restrict__ keys) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= NP) return;
+    if (i >= n) { keys[i] = ~0ull; return; }
+    const int32_t k = key[i];
+    const uint32_t hi = k < 0 ? 0xFFFFFFFEu : (uint32_t)(0x7FFFFFFF - k);
+    keys[i] = ((uint64_t)hi << 32) | (uint32_t)i;
+}
+
+__global__ void lpt_order_kernel(const uint64_t* __restrict__ keys, int n, int32_t* __restrict__ order) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) order[i] = (int32_t)(uint32_t)keys[i];
+}
+
 static int pow2_at_least(int n) {
     int p = 1;
     while (p < n) p <<= 1;
@@ -230,6 +246,23 @@ static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 }  // namespace ttga
 
 using namespace ttga;
+
+// ascending bitonic sort of NP (a power of two) u64 keys on stream st
+static void sort_keys(uint64_t* keys, int NP, hipStream_t st) {
+    if (NP <= 4096) {
+        hipLaunchKernelGGL(bitonic_lds_kernel, dim3(1), dim3(std::min(NP, 1024)), 0, st, keys, NP);
+        return;
+    }
+    // NP / kSortTile tiles: 1 + sum over the stages above the tile of (global steps + 1)
+    // launches (10 at NP = 65,536) instead of one per (k, j) step (136)
+    const int tiles = NP / kSortTile;
+    hipLaunchKernelGGL(bitonic_tile_kernel, dim3(tiles), dim3(1024), 0, st, keys, 0);
+    for (int k = 2 * kSortTile; k <= NP; k <<= 1) {
+        for (int j = k >> 1; j >= kSortTile; j >>= 1)
+            hipLaunchKernelGGL(bitonic_step_kernel, dim3((NP + 255) / 256), dim3(256), 0, st, keys, NP, k, j);
+        hipLaunchKernelGGL(bitonic_tile_kernel, dim3(tiles), dim3(1024), 0, st, keys, k);
+    }
+}
 
 // launched from tt_rooms.hip (masked variants of the matcher and of mutation)
 namespace ttga {
@@ -288,23 +321,28 @@ extern "C" int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* po
     int32_t* wm = (int32_t*)(wr + align256((size_t)N * E));
     hipLaunchKernelGGL(replace_keys_kernel, dim3((NP + 255) / 256), dim3(256), 0, st, pop_penalty, child_penalty, N, C,
                        NP, keys);
-    if (NP <= 4096) {
-        hipLaunchKernelGGL(bitonic_lds_kernel, dim3(1), dim3(std::min(NP, 1024)), 0, st, keys, NP);
-    } else {
-        // NP / kSortTile tiles: 1 + sum over the stages above the tile of (global steps + 1)
-        // launches (10 at NP = 65,536) instead of one per (k, j) step (136)
-        const int tiles = NP / kSortTile;
-        hipLaunchKernelGGL(bitonic_tile_kernel, dim3(tiles), dim3(1024), 0, st, keys, 0);
-        for (int k = 2 * kSortTile; k <= NP; k <<= 1) {
-            for (int j = k >> 1; j >= kSortTile; j >>= 1)
-                hipLaunchKernelGGL(bitonic_step_kernel, dim3((NP + 255) / 256), dim3(256), 0, st, keys, NP, k, j);
-            hipLaunchKernelGGL(bitonic_tile_kernel, dim3(tiles), dim3(1024), 0, st, keys, k);
-        }
-    }
+    sort_keys(keys, NP, st);
     hipLaunchKernelGGL(replace_gather_kernel, dim3(N), dim3(64), 0, st, E, N, C, keys, pop_slot, pop_room, pop_hcv,
                        pop_scv, pop_feasible, pop_penalty, child_slot, child_room, child_hcv, child_scv, child_feasible,
                        child_penalty, ws, wr, wm);
     hipLaunchKernelGGL(replace_scatter_kernel, dim3(N), dim3(64), 0, st, E, ws, wr, wm, pop_slot, pop_room, pop_hcv,
                        pop_scv, pop_feasible, pop_penalty);
     return check_hip(hipGetLastError(), "tt_ga_replace launch");
+}
+
+extern "C" int tt_lpt_order(const tt_problem* p, const int32_t* key, int n, int32_t* order, void* work, void* stream) {
+    if (!p || n < 0 || (n > 0 && (!key || !order || !work))) {
+        set_error("tt_lpt_order: bad arguments");
+        return TT_ERR_INVALID;
+    }
+    if (n == 0) return TT_OK;
+    int rc = use_device(p);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const int NP = pow2_at_least(n);
+    uint64_t* keys = (uint64_t*)work;
+    hipLaunchKernelGGL(lpt_keys_kernel, dim3((NP + 255) / 256), dim3(256), 0, st, key, n, NP, keys);
+    sort_keys(keys, NP, st);
+    hipLaunchKernelGGL(lpt_order_kernel, dim3((n + 255) / 256), dim3(256), 0, st, keys, n, order);
+    return check_hip(hipGetLastError(), "tt_lpt_order launch");
 }

@@ -382,6 +382,8 @@ struct Island {
     int64_t *rng_init = nullptr, *rng_child = nullptr;
     uint8_t* flags = nullptr;
     void* work = nullptr;
+    int32_t* order = nullptr;                         // LPT dispatch order (C >= kLptMinChildren)
+    static constexpr int kLptMinChildren = 4096;      // as ttga.ga.Island
     // migrants (ga.cpp:318-335): slot[E] room[E] hcv scv penalty feasible
     uint8_t *send_best = nullptr, *send_second = nullptr, *recv_buf = nullptr;
     size_t migrant_bytes = 0;
@@ -403,6 +405,7 @@ struct Island {
         check_hip(hipMemcpy(rng_init, s.data(), 8 * (size_t)N, hipMemcpyHostToDevice), "hipMemcpy");
         check_hip(hipMemcpy(rng_child, s.data() + N, 8 * (size_t)C, hipMemcpyHostToDevice), "hipMemcpy");
         check_hip(hipMalloc(&flags, (size_t)C), "hipMalloc");
+        if (C >= kLptMinChildren) check_hip(hipMalloc(&order, 4 * (size_t)C), "hipMalloc");
         check_hip(hipMalloc(&work, std::max<size_t>(tt_ga_work_bytes(N, E), 16)), "hipMalloc");
         migrant_bytes = 2 * (size_t)E + 13;
         check_hip(hipMalloc(&send_best, migrant_bytes), "hipMalloc");
@@ -429,8 +432,17 @@ struct Island {
         check_tt(tt_ga_breed(tp, pop.slot, pop.room, pop.penalty, N, rng_child, C, p_cross, p_mut, 1, child.slot,
                              child.room, flags, st),
                  "tt_ga_breed");
-        check_tt(tt_local_search(tp, child.slot, child.room, rng_child, C, max_steps, p1, p2, p3, st),
-                 "tt_local_search");
+        if (order) {
+            // longest-expected first: the children's hcv before the search, descending
+            // (a generation's search launch ends with its slowest children); same results
+            evaluate(child);
+            check_tt(tt_lpt_order(tp, child.hcv, C, order, work, st), "tt_lpt_order");
+            check_tt(tt_local_search_ordered(tp, child.slot, child.room, rng_child, C, max_steps, p1, p2, p3, order, st),
+                     "tt_local_search_ordered");
+        } else {
+            check_tt(tt_local_search(tp, child.slot, child.room, rng_child, C, max_steps, p1, p2, p3, st),
+                     "tt_local_search");
+        }
         evaluate(child);
         check_tt(tt_ga_replace(tp, pop.slot, pop.room, pop.hcv, pop.scv, pop.feasible, pop.penalty, N, child.slot,
                                child.room, child.hcv, child.scv, child.feasible, child.penalty, C, work, st),
@@ -496,8 +508,8 @@ struct Island {
     void release() {
         pop.release();
         child.release();
-        for (void* p : {(void*)rng_init, (void*)rng_child, (void*)flags, work, (void*)send_best, (void*)send_second,
-                        (void*)recv_buf})
+        for (void* p : {(void*)rng_init, (void*)rng_child, (void*)flags, work, (void*)order, (void*)send_best,
+                        (void*)send_second, (void*)recv_buf})
             if (p) (void)hipFree(p);
         if (st) (void)hipStreamDestroy(st);
         if (tp) tt_problem_destroy(tp);

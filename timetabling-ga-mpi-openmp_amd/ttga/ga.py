@@ -174,7 +174,6 @@ class Island(Members):
 
     def step(self):
         """One generation of C children (ga.cpp:543-585)."""
-        import torch
         c = self.child
         self.dp.ga_breed(self.pop["slot"], self.pop["room"], self.pop["penalty"], self.rng_child, c["slot"], c["room"],
                          self.flags, self.p_cross, self.p_mut, self.skip)
@@ -183,7 +182,7 @@ class Island(Members):
             # dispatch the children longest-expected first (hcv before the search,
             # descending): the launch's tail is its slowest waves; results unchanged
             self._evaluate(c)
-            order = torch.argsort(c["hcv"], descending=True, stable=True).to(torch.int32)
+            order = self.dp.lpt_order(c["hcv"], self.work)
         self.dp.local_search(c["slot"], c["room"], self.rng_child, self.max_steps, self.p1, self.p2, self.p3,
                              order=order)
         self._evaluate(c)

@@ -23,7 +23,7 @@ EXPORTS = (
     "tt_problem_create", "tt_problem_destroy", "tt_problem_dims", "tt_problem_derived", "tt_eval",
     "tt_eval_variant", "tt_assign_rooms", "tt_random_init", "tt_crossover", "tt_mutation", "tt_local_search",
     "tt_device_status", "tt_last_error", "tt_version", "tt_ga_breed", "tt_ga_work_bytes", "tt_ga_replace",
-    "tt_eval_auto_variant", "tt_local_search_ordered",
+    "tt_eval_auto_variant", "tt_local_search_ordered", "tt_lpt_order",
 )
 
 _lib = None
@@ -58,6 +58,7 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.tt_mutation.argtypes = [vp, vp, vp, vp, i32, vp]
     lib.tt_local_search.argtypes = [vp, vp, vp, vp, i32, i32, dbl, dbl, dbl, vp]
     lib.tt_local_search_ordered.argtypes = [vp, vp, vp, vp, i32, i32, dbl, dbl, dbl, vp, vp]
+    lib.tt_lpt_order.argtypes = [vp, vp, i32, vp, vp, vp]
     lib.tt_device_status.argtypes = [vp, vp]
     lib.tt_eval_auto_variant.argtypes = [vp]
     lib.tt_ga_breed.argtypes = [vp, vp, vp, vp, i32, vp, i32, dbl, dbl, i32, vp, vp, vp, vp]
@@ -201,6 +202,19 @@ class DeviceProblem:
                                                           rng.data_ptr(), P, int(max_steps), float(p1), float(p2),
                                                           float(p3), ctypes.c_void_p(order.data_ptr()),
                                                           self._stream(slot)))
+
+    def lpt_order(self, key, work):
+        """tt_lpt_order: indices of key (int32 CUDA) by key descending, ties by
+        index, negative keys last, as an int32 CUDA tensor."""
+        import torch
+        n = key.numel()
+        if not (key.is_cuda and key.dtype == torch.int32 and key.is_contiguous()):
+            raise ValueError("key must be a contiguous int32 CUDA tensor")
+        order = torch.empty(n, dtype=torch.int32, device=key.device)
+        _check(self.lib, self.lib.tt_lpt_order(self.handle, ctypes.c_void_p(key.data_ptr()), n,
+                                               ctypes.c_void_p(order.data_ptr()), ctypes.c_void_p(work.data_ptr()),
+                                               self._stream(key)))
+        return order
 
     # -- GA generation primitives ---------------------------------------------------
     def ga_breed(self, pop_slot, pop_room, pop_penalty, rng, child_slot, child_room, child_flags,
