@@ -1,3 +1,6 @@
+#!/bin/bash
+# LPT A/B for the phase-2 GA bench (8,192 and 32,768 children) after the GA/LS parity tests.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 set -u
 export TMPDIR=/tmp
 O=gpurun_out/s3lpt; mkdir -p $O
