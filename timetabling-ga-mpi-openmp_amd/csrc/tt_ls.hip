@@ -1220,6 +1220,9 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
         return check_hip(hipGetLastError(), "local_search launch");
     }
     const LsLayout Ls = ls_layout(p->E, p->R, p->dev.EW64, kLsCapSmall);
+    // per-call flags from the stream-ordered pool (hipMallocAsync reuses freed
+    // blocks; a buffer cached in the handle would race when one handle serves
+    // several streams, which the C-ABI allows)
     uint8_t* redo = nullptr;
     TT_HIP(hipMallocAsync((void**)&redo, (size_t)P, st));
     TT_HIP(hipMemsetAsync(redo, 0, (size_t)P, st));
