@@ -744,7 +744,10 @@ __device__ __forceinline__ int window_resolve(int lane, uint32_t jump, int64_t& 
 // individual that overflowed a task, whose HBM row and stream are then left
 // as they were. redo_in (second launch): only flagged individuals run.
 template <int CAP>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void local_search_kernel(DevProblem pb, uint8_t* __restrict__ slot,
+#ifndef TT_LS_WPE
+#define TT_LS_WPE 5
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE))) void local_search_kernel(DevProblem pb, uint8_t* __restrict__ slot,
                                                           uint8_t* __restrict__ room, int64_t* __restrict__ rng,
                                                           int P, int max_steps, double p1, double p2, double p3,
                                                           uint8_t* __restrict__ redo_out,
