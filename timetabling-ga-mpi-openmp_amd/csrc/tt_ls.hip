@@ -30,6 +30,12 @@ constexpr int kLsTasks = 3;
 // input by the second launch with tasks sized for kMaxSlotEvents.
 constexpr int kLsCapSmall = 64;
 
+// ballots per block of the wave matcher's room transpose (4: fewer wasted
+// ballots past R; same results, A/B in tools/ab_ls.py)
+#ifndef TT_LS_TRU
+#define TT_LS_TRU 4
+#endif
+
 // Profiling build (-DTT_LS_PROF, `make libttga_prof.so`, tools/ls_prof.py):
 // per-section shader-clock totals of every wave, summed into g_ls_prof.
 #ifdef TT_LS_PROF
@@ -239,9 +245,9 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
     // transpose: ev_of_room (lane j) = the events whose possible rooms include j
     // (8 independent ballots per block; pl has no bits at or above R)
     uint64_t eor = 0;
-    for (int j0 = 0; j0 < R; j0 += 8) {
+    for (int j0 = 0; j0 < R; j0 += TT_LS_TRU) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
+        for (int q = 0; q < TT_LS_TRU; ++q) {
             const uint64_t b = __ballot(act && ((pl >> (j0 + q)) & 1ull));
             if (lane == j0 + q) eor = b;
         }
@@ -305,31 +311,34 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
     // free possible room, else the first possible room; one with no possible room
     // keeps lessBusy carried over from the previous unplaced event (initially 0)
     const bool un = act && mr == NONE;
-    uint32_t v = 0;
-    if (un && pl) {
-        v = (uint32_t)__builtin_ctzll(pl);
-        if ((rmatched >> v) & 1ull) {
-            const uint64_t fr2 = pl & ~rmatched;
-            if (fr2) v = (uint32_t)__builtin_ctzll(fr2);
+    const uint64_t unb = __ballot(un);
+    uint32_t r = mr;
+    if (unb) {                                     // wave-uniform: usually every event is placed
+        uint32_t v = 0;
+        if (un && pl) {
+            v = (uint32_t)__builtin_ctzll(pl);
+            if ((rmatched >> v) & 1ull) {
+                const uint64_t fr2 = pl & ~rmatched;
+                if (fr2) v = (uint32_t)__builtin_ctzll(fr2);
+            }
         }
+        const uint64_t carriers = __ballot(un && pl != 0ull);
+        const uint64_t below = carriers & ((1ull << lane) - 1ull);
+        const int src = below ? 63 - __builtin_clzll(below) : lane;
+        const uint32_t carried = (uint32_t)__shfl((int)v, src, 64);
+        r = !un ? mr : (pl ? v : (below ? carried : 0u));
     }
-    const uint64_t carriers = __ballot(un && pl != 0ull);
-    const uint64_t below = carriers & ((1ull << lane) - 1ull);
-    const int src = below ? 63 - __builtin_clzll(below) : lane;
-    const uint32_t carried = (uint32_t)__shfl((int)v, src, 64);
-    const uint32_t r = !un ? mr : (pl ? v : (below ? carried : 0u));
-    // room histogram (lane j = room j) and the pairs of events sharing a room,
-    // from one ballot per room (r < R for every event)
+    // room histogram (lane j = room j) and the pairs of events sharing a room
+    // (r < R for every event): matched events hold distinct rooms, the rooms in
+    // rmatched, so only the unplaced events add to a room's count and make pairs
     const LsTask T = get_task(S, k);
-    uint32_t cnt_r = 0;
+    uint32_t cnt_r = (uint32_t)((rmatched >> lane) & 1ull);
     int pr = 0;
-    for (int j0 = 0; j0 < R; j0 += 8) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int c = __popcll(__ballot(act && r == (uint32_t)(j0 + q)));
-            pr += c * (c - 1) / 2;
-            if (lane == j0 + q) cnt_r = (uint32_t)c;
-        }
+    for (uint64_t um = unb; um; um &= um - 1) {
+        const int i = __builtin_ctzll(um);
+        const int ri = __builtin_amdgcn_readlane((int)r, i);
+        pr += __builtin_amdgcn_readlane((int)cnt_r, ri);
+        if (lane == ri) ++cnt_r;
     }
     if (act) S.nrr[ev] = (uint8_t)r;
     if (lane < R) T.hist[lane] = (uint16_t)cnt_r;
