@@ -243,12 +243,12 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
     const bool act = lane < N;
     const uint32_t pl_lo = (uint32_t)pl, pl_hi = (uint32_t)(pl >> 32);
     // transpose: ev_of_room (lane j) = the events whose possible rooms include j
-    // (8 independent ballots per block; pl has no bits at or above R)
+    // (TT_LS_TRU independent ballots per block; pl has no bits at or above R)
     uint64_t eor = 0;
     for (int j0 = 0; j0 < R; j0 += TT_LS_TRU) {
 #pragma unroll
         for (int q = 0; q < TT_LS_TRU; ++q) {
-            const uint64_t b = __ballot(act && ((pl >> (j0 + q)) & 1ull));
+            const uint64_t b = __ballot((pl >> (j0 + q)) & 1ull);   // pl is zero past the N events (load_tasks)
             if (lane == j0 + q) eor = b;
         }
     }

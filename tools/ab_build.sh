@@ -16,8 +16,9 @@ fi
 mkdir -p "$SRC/obj"
 for f in "$SRC"/x/csrc/*.hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC ${HIPX:-} -c "$f" -o "$SRC/obj/$(basename "$f" .hip).o" &
+  pids="${pids:-} $!"
 done
-wait
+for p in $pids; do wait $p || { echo "compile failed" >&2; rm -rf "$SRC"; exit 1; }; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$REPO/ab_libs/libttga_$NAME.so" "$SRC"/obj/*.o
 rm -rf "$SRC"
 echo "$REPO/ab_libs/libttga_$NAME.so"
