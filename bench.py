@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warm-seconds", type=float, default=0.25,
+                    help="keep warming up until this much wall time of launches has run")
     ap.add_argument("--pop", type=int, default=POP_PER_GPU)
     ap.add_argument("--config", default="med", choices=["sm", "med", "lg", "syn"])
     ap.add_argument("--variant", type=int, default=0, help="tt_eval kernel: 0 auto, 2 block, 7/8 tile5, 13 wide path")
@@ -122,10 +124,17 @@ def main():
         # live counters of the same workload, before this process initialises the GPU
         sys.path.insert(0, str(REPO / "tools"))
         import pmc_live
+        v = args.variant or (8 if args.config != "syn" else 13)
         child = [str(REPO / "bench.py"), "--pmc-child", "--config", args.config, "--pop", str(args.pop),
-                 "--steps", "20", "--warmup", "2", "--variant", str(args.variant)]
-        pmc = pmc_live.derive(pmc_live.collect(child, DOMINANT.get(args.variant or
-                                                                   (8 if args.config != "syn" else 13), "eval_")))
+                 "--steps", "20", "--warmup", "2", "--variant", str(v)]
+        # FETCH_SIZE read-factor calibration: the same kernel with its evaluation phases
+        # off (tile5: lane and wave phase; wide path: eval_lanes only), which reads
+        # exactly the P*E bytes of the slot rows with the kernel's own loads
+        calib = list(child)
+        calib[-1] = str(v | (0x30 if v in (7, 8) else 0x40 if v == 13 else 0))
+        E = {"sm": 100, "syn": 2000}.get(args.config, 400)
+        pmc = pmc_live.derive(pmc_live.collect(child, DOMINANT.get(v, "eval_"), calib if v in (7, 8, 13) else None),
+                              calib_bytes=float(args.pop) * E)
     import torch
     import torch.distributed as dist
 
@@ -159,9 +168,15 @@ def main():
            torch.empty(P, dtype=torch.uint8, device=dev), torch.empty(P, dtype=torch.int32, device=dev))
     torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
-        dp.eval(slot, room, variant=args.variant, out=out)
-    torch.cuda.synchronize(dev)
+    # warm-up: W launches, then more until >= WARM_S of launches have run, so the
+    # timed steps see settled clocks (outside the timed region)
+    t_w = time.perf_counter()
+    launched = 0
+    while launched < args.warmup or time.perf_counter() - t_w < args.warm_seconds:
+        for _ in range(max(1, min(args.warmup, 50)) if launched < args.warmup else 50):
+            dp.eval(slot, room, variant=args.variant, out=out)
+            launched += 1
+        torch.cuda.synchronize(dev)
 
     stream = torch.cuda.current_stream(dev)      # tt_eval launches its one kernel on this stream
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -194,7 +209,7 @@ def main():
         variant = args.variant or dp.eval_variant()
         line = {
             "metric": METRIC, "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": wall_max / args.steps * 1e3, "higher_is_better": True,
+            "warmup": args.warmup, "warmup_launches": launched, "ms_per_step": wall_max / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "i32", "data": "synthetic",
             "config": {"workload": f"{args.config} instance E={E} R={inst.R} F={inst.F} S={inst.S} (seeded synthetic, "
                                    f"{SIZE_NAMES[args.config]}), population {P} per GPU, one tt_eval (hcv+scv+feasible+penalty) "
@@ -204,7 +219,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": None if pmc is None else pmc["traffic_bytes"],
-                         "traffic_unit": "bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, live rocprofv3 pass)",
+                         "traffic_unit": "bytes per launch (FETCH_SIZE x calibrated read factor + WRITE_SIZE, "
+                                         "live rocprofv3 passes; see traffic_detail)",
                          "algorithmic_bytes": bytes_per_eval * P,
                          "kernel_ms": kernel_ms, "bytes_per_eval": bytes_per_eval},
         }
@@ -212,6 +228,9 @@ def main():
             line["config"]["rehearsal"] = (f"{world} ranks on {torch.cuda.device_count()} GPU(s), {backend} "
                                            f"process group: checks the multi-rank path, not a scaling number")
         if pmc is not None:
+            line["roofline"]["traffic_detail"] = {k: pmc.get(k) for k in ("fetch_kib", "write_kib", "fetch_factor",
+                                                                          "fetch_factor_how", "calib_fetch_kib",
+                                                                          "calib_bytes")}
             line["roofline"]["pipes"] = {k: pmc[k] for k in ("lds_busy", "lds_conflict", "valu_busy", "salu_busy",
                                                             "wait_any", "cycles") if k in pmc}
         if world == 1 and not args.no_cpu:

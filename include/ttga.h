@@ -119,7 +119,8 @@ int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* 
 /* tt_local_search with the individuals dispatched in the order order[0..P-1]
  * (device i32, a permutation of 0..P-1; NULL: 0..P-1). Every individual's
  * result is the same as tt_local_search's; only the wave launch order changes
- * (longest-expected first shortens the launch's tail). */
+ * (longest-expected first shortens the launch's tail). An order that is not a
+ * permutation sets tt_device_status bit 3. */
 int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P, int max_steps,
                             double p1, double p2, double p3, const int32_t* order, void* stream);
 
@@ -146,8 +147,16 @@ int tt_ga_breed(const tt_problem* p, const uint8_t* pop_slot, const uint8_t* pop
                 int N, int64_t* rng, int C, double p_cross, double p_mut, int skip_init_draws, uint8_t* child_slot,
                 uint8_t* child_room, uint8_t* child_flags, void* stream);
 
-/* Bytes of device scratch tt_ga_replace needs for a population of N. */
+/* Bytes of device scratch tt_ga_replace needs for a population of N (also
+ * enough for tt_lpt_order over n <= N keys). */
 size_t tt_ga_work_bytes(int N, int E);
+
+/* Byte offset, inside a tt_ga_work_bytes(N, E) work buffer, of the int32 that
+ * tt_ga_replace leaves there: the merged position the new pop[0] came from
+ * (N-C+c for child c, else its old position), which the drivers report as
+ * the logEntry threadID (ga.cpp:498,580-585). Only tt_ga_replace writes it;
+ * tt_lpt_order and the rest of the scratch never touch it. */
+size_t tt_ga_work_source_offset(int N, int E);
 
 /* tt_ga_replace: the C evaluated children overwrite population positions
  * N-C..N-1 (ga.cpp:582, "pop[popSize-1]->copy(child)" for C = 1), then the
@@ -155,9 +164,8 @@ size_t tt_ga_work_bytes(int N, int E);
  * order, std::sort leaves them unspecified). Penalties compare as unsigned,
  * so an invalid genome (penalty -1) sorts last; tt_ga_breed's selection5
  * ranks it last the same way. In place; `work` has tt_ga_work_bytes(N, E)
- * bytes. On return the first 8 bytes of `work` hold the sort key of the new
- * pop[0]: its low 32 bits are the merged position it came from (N-C+c for
- * child c), which the drivers use as the logEntry threadID. */
+ * bytes. On return the int32 at tt_ga_work_source_offset(N, E) holds the
+ * merged position the new pop[0] came from (N-C+c for child c). */
 int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* pop_room, int32_t* pop_hcv, int32_t* pop_scv,
                   uint8_t* pop_feasible, int32_t* pop_penalty, int N, const uint8_t* child_slot,
                   const uint8_t* child_room, const int32_t* child_hcv, const int32_t* child_scv,
@@ -171,7 +179,12 @@ int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* pop_room, int
  *              counts towards evCount < E or accepts a move, which costs a step,
  *              so a phase makes at most (maxSteps + 2) * E visits
  *              (Solution.cpp:498-505,616-618) and the bound is twice that per
- *              phase; tests assert it never fires.
+ *              phase; tests assert it never fires;
+ *   bit 3 (8)  tt_local_search_ordered got a dispatch order that is not a
+ *              permutation of 0..P-1 (an entry out of range, or a duplicate with
+ *              an entry missing: checked on the device by range, sum and sum of
+ *              squares); out-of-range entries are skipped, a duplicated
+ *              individual is searched twice concurrently (undefined result).
  * Synchronises the device. */
 int tt_device_status(const tt_problem* p, int32_t* status);
 

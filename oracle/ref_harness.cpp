@@ -251,18 +251,31 @@ void ref_mutation(void* p, u8* slot, u8* room, long* rng, int np) {
 // solution (F2: its timeslot lists then hold every event twice, which slows
 // the matching and the local search); as_is = 0: crossover into a fresh
 // Solution, the semantics the device engine implements.
-// Only the time is of interest (bench CPU baseline). Returns seconds.
-double ref_ga_children_timed(void* p, const u8* pop_slot, const u8* pop_room, const int* pop_penalty, int N,
-                             long* rng, int C, int max_steps, int threads, int as_is) {
+// The parents are loaded with all 45 timeslot keys present, as every member
+// of the reference's population has them (RandomInitialSolution touches each
+// key, Solution.cpp:56-59), so copy() replaces every list of cp1/cp2.
+// Outputs (any may be NULL): the child's slot/room rows, hcv, scv, feasible
+// and penalty (computed after the clock stops) and its final RNG state.
+// Returns the seconds of the per-child work.
+double ref_ga_children(void* p, const u8* pop_slot, const u8* pop_room, const int* pop_penalty, int N, long* rng,
+                       int C, int max_steps, int threads, int as_is, u8* out_slot, u8* out_room, int* out_hcv,
+                       int* out_scv, u8* out_feasible, int* out_penalty) {
     Problem* P = (Problem*)p;
     const int E = P->n_of_events;
+    const bool keep = out_slot || out_room || out_hcv || out_scv || out_feasible || out_penalty;
+    std::vector<Solution*> kept(keep ? C : 0, (Solution*)0);
+    std::vector<Solution*> owned(keep ? 3 * (long)C + C : 0, (Solution*)0);
+    std::vector<Random*> rngs(C, (Random*)0);
+    for (int c = 0; c < C; c++) {
+        rngs[c] = new Random(0);
+        rngs[c]->seed = rng[c];
+    }
     omp_set_num_threads(threads);
     struct timeval t0, t1;
     gettimeofday(&t0, 0);
 #pragma omp parallel for schedule(dynamic, 1)
     for (int c = 0; c < C; c++) {
-        Random r(0);
-        r.seed = rng[c];
+        Random& r = *rngs[c];
         Solution* child = new Solution(P, &r);
         child->RandomInitialSolution();
         Solution* cp1 = new Solution(P, &r);
@@ -281,26 +294,57 @@ double ref_ga_children_timed(void* p, const u8* pop_slot, const u8* pop_room, co
         Solution a(P, &r), b(P, &r);
         load_solution(&a, pop_slot + (long)sel[0] * E, pop_room + (long)sel[0] * E, E);
         load_solution(&b, pop_slot + (long)sel[1] * E, pop_room + (long)sel[1] * E, E);
+        for (int t = 0; t < 45; t++) {
+            a.timeslot_events[t];
+            b.timeslot_events[t];
+        }
         cp1->copy(&a);
         cp2->copy(&b);
         Solution* use = child;
-        Solution fresh(P, &r);
+        Solution* fresh = new Solution(P, &r);
         if (r.next() < 0.8) {
             if (as_is) child->crossover(cp1, cp2);
-            else { fresh.crossover(cp1, cp2); use = &fresh; }
+            else { fresh->crossover(cp1, cp2); use = fresh; }
         } else {
             use = cp1;
         }
         if (r.next() < 0.5) use->mutation();
         use->localSearch(max_steps);
         use->computePenalty();
-        rng[c] = r.seed;
-        delete child;
-        delete cp1;
-        delete cp2;
+        if (keep) {
+            kept[c] = use;
+            owned[4L * c] = child; owned[4L * c + 1] = cp1; owned[4L * c + 2] = cp2; owned[4L * c + 3] = fresh;
+        } else {
+            delete child;
+            delete cp1;
+            delete cp2;
+            delete fresh;
+        }
     }
     gettimeofday(&t1, 0);
+    for (int c = 0; c < C; c++) {
+        rng[c] = rngs[c]->seed;
+        if (keep) {
+            Solution* s = kept[c];
+            store_solution(s, out_slot ? out_slot + (long)c * E : 0, out_room ? out_room + (long)c * E : 0, E);
+            const bool f = s->computeFeasibility();
+            const int h = s->computeHcv(), v = s->computeScv();
+            if (out_hcv) out_hcv[c] = h;
+            if (out_scv) out_scv[c] = v;
+            if (out_feasible) out_feasible[c] = f ? 1 : 0;
+            if (out_penalty) out_penalty[c] = s->penalty;
+        }
+        delete rngs[c];
+    }
+    for (size_t k = 0; k < owned.size(); k++) delete owned[k];
     return (t1.tv_sec - t0.tv_sec) + 1e-6 * (t1.tv_usec - t0.tv_usec);
+}
+
+// ref_ga_children without outputs: the bench's CPU baseline (seconds).
+double ref_ga_children_timed(void* p, const u8* pop_slot, const u8* pop_room, const int* pop_penalty, int N,
+                             long* rng, int C, int max_steps, int threads, int as_is) {
+    return ref_ga_children(p, pop_slot, pop_room, pop_penalty, N, rng, C, max_steps, threads, as_is, 0, 0, 0, 0, 0,
+                           0);
 }
 
 static bool by_penalty(Solution* a, Solution* b) { return a->penalty < b->penalty; }   // ga.cpp:150-153

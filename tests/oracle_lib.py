@@ -10,7 +10,9 @@ Both expose the same batched API over numpy arrays so tests can run either.
 from __future__ import annotations
 
 import ctypes
+import os
 import pathlib
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -188,3 +190,49 @@ def _ga_run(self, seeds, pop_size=10, gens=2001, max_steps=200, as_is=1, threads
 
 
 _Handle.ga_run = _ga_run
+
+
+def _ga_children(self, pop_slot, pop_room, pop_penalty, seeds, max_steps, threads=1, as_is=0):
+    """ref_ga_children: the reference's per-child path of ga.cpp:543-577 (Ref
+    only), child c on Random(seeds[c]). Returns (dict of the children's slot,
+    room, hcv, scv, feasible, penalty; final streams; seconds)."""
+    pop_slot = np.ascontiguousarray(pop_slot, np.uint8); pop_room = np.ascontiguousarray(pop_room, np.uint8)
+    pen = np.ascontiguousarray(pop_penalty, np.int32)
+    rng = np.ascontiguousarray(seeds, np.int64).copy()
+    C, N = rng.size, pop_slot.shape[0]
+    out = dict(slot=np.zeros((C, self.E), np.uint8), room=np.zeros((C, self.E), np.uint8),
+               hcv=np.zeros(C, np.int32), scv=np.zeros(C, np.int32), feasible=np.zeros(C, np.uint8),
+               penalty=np.zeros(C, np.int32))
+    fn = self.c._f("ga_children")
+    fn.restype = ctypes.c_double
+    fn.argtypes = [_vp] * 4 + [ctypes.c_int, _vp] + [ctypes.c_int] * 4 + [_vp] * 6
+    secs = fn(self.h, _p(pop_slot), _p(pop_room), _p(pen), N, _p(rng), C, int(max_steps), int(threads), int(as_is),
+              _p(out["slot"]), _p(out["room"]), _p(out["hcv"]), _p(out["scv"]), _p(out["feasible"]),
+              _p(out["penalty"]))
+    return out, rng, secs
+
+
+_Handle.ga_children = _ga_children
+
+
+def host_threads(cap: int = 16) -> int:
+    """Threads for the checkers: the cores this job may use, at most `cap`
+    (the GPU box grants 16; os.cpu_count() there shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(cap, n))
+
+
+def split_rows(fn, arrays, *args, threads: int | None = None):
+    """fn(*row_slices, *args) over contiguous row blocks of `arrays` on host
+    threads (ctypes releases the GIL; the checkers keep no shared mutable
+    state), the per-block result tuples concatenated row-wise. Results equal
+    one serial call: every individual carries its own stream."""
+    n = arrays[0].shape[0]
+    T = threads or host_threads()
+    blocks = [b for b in np.array_split(np.arange(n), min(T, max(n, 1))) if b.size]
+    with ThreadPoolExecutor(len(blocks)) as ex:
+        parts = list(ex.map(lambda b: fn(*(np.ascontiguousarray(a[b]) for a in arrays), *args), blocks))
+    return tuple(np.concatenate(x) for x in zip(*parts))

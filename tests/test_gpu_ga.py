@@ -256,3 +256,47 @@ def test_breed_selection5_vs_reference(sm, c):
             pm.next()
         take_a = np.array([pm.next() < 0.5 for _ in range(inst.E)])
         assert np.array_equal(got[k], np.where(take_a, pop_slot[w[2 * k]], pop_slot[w[2 * k + 1]])), k
+
+
+def test_best_thread_with_lpt_dispatch(sm):
+    """The logEntry threadID (Island.best_thread, from the source slot
+    tt_ga_replace writes at tt_ga_work_source_offset) with LPT dispatch on
+    (C >= 4096, tt_lpt_order sorts in the same work buffer): after each
+    generation it names the child that became pop[0], or 0 when the old pop[0]
+    stayed (it wins ties: lower merged position)."""
+    inst, dp, o = sm
+    N, C = 8192, 4096
+    isl = Island(dp, pop_size=N, children=C, max_steps=50, seed=12)
+    assert isl.lpt
+    isl.initialize()
+    changed = 0
+    for _ in range(4):
+        old0 = int(host(isl.pop["penalty"])[0])
+        isl.step()
+        cpen = host(isl.child["penalty"]).astype(np.uint32)
+        c = int(np.argmin(cpen))
+        exp = c if cpen[c] < np.uint32(old0) else 0
+        got = isl.best_thread()
+        assert got == exp
+        if cpen[c] < np.uint32(old0):
+            changed += 1
+            assert np.array_equal(host(isl.pop["slot"][0]), host(isl.child["slot"][c]))
+    assert changed > 0
+
+
+def test_local_search_order_permutation_check():
+    """tt_local_search_ordered flags a dispatch order that is not a
+    permutation (status bit 3): a duplicate entry (one individual missing), an
+    out-of-range entry; a true permutation leaves the status clean."""
+    inst = ttga.config_instance("med")
+    P = 64
+    seeds = ttga.population_seeds(31, P)
+    for order, bad in ((np.random.default_rng(0).permutation(P), False),
+                       (np.r_[np.arange(P - 1), 0], True),
+                       (np.r_[np.arange(P - 1), P], True)):
+        dp = native.DeviceProblem(inst)
+        s = dev(ttga.random_slots(seeds, inst.E)[0])
+        r = dp.assign_rooms(s)
+        dp.local_search(s, r, dev(seeds), 50, order=dev(order.astype(np.int32)))
+        assert bool(dp.status() & 8) == bad, order[-3:]
+        dp.close()

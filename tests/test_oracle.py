@@ -166,3 +166,29 @@ def test_oracle_vs_reference_med_ls_chain(orc):
             assert np.array_equal(x, y), steps
     for x, y in zip(ho.eval(a[0], a[1]), hr.eval(b[0], b[1])):
         assert np.array_equal(x, y)
+
+
+@needs_ref
+@pytest.mark.parametrize("name,steps", [("sm", 200), ("comp01", 200)])
+def test_oracle_children_vs_reference_per_child_path(orc, name, steps):
+    """The oracle's generation primitives (ga_breed with the 3E discarded draws,
+    local_search, eval) equal the reference's own per-child path of
+    ga.cpp:543-577 (oracle/_ref ref_ga_children: three RandomInitialSolution,
+    two selection5, copies, crossover into a fresh child or copy, mutation,
+    localSearch, computePenalty) child for child on the same streams."""
+    from ttga.ga import stream_seeds
+    inst = ttga.config_instance(name)
+    ho, hr = orc.problem(inst), REF.problem(inst)
+    N, C = 24, 24
+    s, r, g = ho.random_init(stream_seeds(11, 0, N))
+    s, r, g = ho.local_search(s, r, g, 100)
+    h, sc, f, pen = ho.eval(s, r)
+    seeds = stream_seeds(11, N, C)
+    cs, cr, fl, rng = ho.ga_breed(s, r, pen, seeds, C, 0.8, 0.5, 1)
+    assert (fl & 1).any() and (fl & 1 == 0).any() and (fl & 2).any()     # both crossover and copy children
+    cs, cr, rng = ho.local_search(cs, cr, rng, steps)
+    exp = dict(zip(("hcv", "scv", "feasible", "penalty"), ho.eval(cs, cr)), slot=cs, room=cr)
+    got, grng, _ = hr.ga_children(s, r, pen, seeds, steps, threads=4)
+    for k, v in exp.items():
+        assert np.array_equal(got[k], v), k
+    assert np.array_equal(grng, rng)

@@ -180,9 +180,10 @@ __global__ __launch_bounds__(64) void replace_gather_kernel(int E, int N, int C,
                                                             const int32_t* __restrict__ ch, const int32_t* __restrict__ csc,
                                                             const uint8_t* __restrict__ cf, const int32_t* __restrict__ cp,
                                                             uint8_t* __restrict__ ws, uint8_t* __restrict__ wr,
-                                                            int32_t* __restrict__ wm) {
+                                                            int32_t* __restrict__ wm, int32_t* __restrict__ best_src) {
     const int i = blockIdx.x;
     const int src = (int)(keys[i] & 0xFFFFFFFFu);
+    if (i == 0 && threadIdx.x == 0) *best_src = src;          // the new pop[0]'s merged position
     const int k = N - C;
     const bool child = src >= k;
     const int r = child ? src - k : src;
@@ -293,10 +294,21 @@ extern "C" int tt_ga_breed(const tt_problem* p, const uint8_t* pop_slot, const u
     return launch_mutation_masked(p, child_slot, child_room, rng, C, child_flags, kFlagMutate, st);
 }
 
-extern "C" size_t tt_ga_work_bytes(int N, int E) {
-    if (N < 1 || E < 1) return 0;
+// work layout: sort keys [pow2(N)] u64 | slot rows [N][E] | room rows [N][E] |
+// meta [N][4] i32 | the source slot (256 B, written only by tt_ga_replace)
+static size_t work_source_offset(int N, int E) {
     const size_t NP = (size_t)pow2_at_least(N);
     return align256(8 * NP) + 2 * align256((size_t)N * E) + align256(16 * (size_t)N);
+}
+
+extern "C" size_t tt_ga_work_bytes(int N, int E) {
+    if (N < 1 || E < 1) return 0;
+    return work_source_offset(N, E) + 256;
+}
+
+extern "C" size_t tt_ga_work_source_offset(int N, int E) {
+    if (N < 1 || E < 1) return 0;
+    return work_source_offset(N, E);
 }
 
 extern "C" int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* pop_room, int32_t* pop_hcv,
@@ -324,7 +336,7 @@ extern "C" int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* po
     sort_keys(keys, NP, st);
     hipLaunchKernelGGL(replace_gather_kernel, dim3(N), dim3(64), 0, st, E, N, C, keys, pop_slot, pop_room, pop_hcv,
                        pop_scv, pop_feasible, pop_penalty, child_slot, child_room, child_hcv, child_scv, child_feasible,
-                       child_penalty, ws, wr, wm);
+                       child_penalty, ws, wr, wm, (int32_t*)(w + work_source_offset(N, E)));
     hipLaunchKernelGGL(replace_scatter_kernel, dim3(N), dim3(64), 0, st, E, ws, wr, wm, pop_slot, pop_room, pop_hcv,
                        pop_scv, pop_feasible, pop_penalty);
     return check_hip(hipGetLastError(), "tt_ga_replace launch");

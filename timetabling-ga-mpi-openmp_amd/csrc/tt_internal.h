@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -18,6 +19,17 @@ struct tt_problem {
     // device allocations
     void* dev_block;
     ttga::DevProblem dev;
+    // local search redo lists, one per stream (count, done counter, entries):
+    // zeroed once when allocated, reset on the device by the redo launch;
+    // ls_mu is held while a call enqueues its launches, so two host threads on
+    // one stream cannot interleave their first and redo launches
+    struct LsRedo {
+        void* stream;
+        int32_t* list;
+        int cap;
+    };
+    std::vector<LsRedo> ls_redo;
+    std::mutex ls_mu;
 };
 
 namespace ttga {

@@ -749,25 +749,19 @@ __device__ __forceinline__ int window_resolve(int lane, uint32_t jump, int64_t& 
     return kstar;
 }
 
-// CAP = matcher task capacity. redo_out (first launch): set to 1 for an
-// individual that overflowed a task, whose HBM row and stream are then left
-// as they were. redo_in (second launch): only flagged individuals run.
+// One individual's localSearch by the calling wave (every lane). CAP =
+// matcher task capacity. redo_list (first launch, CAP = kLsCapSmall): an
+// individual that overflowed a task is appended to it (redo_list[0] counts,
+// entries from redo_list[2]) and its HBM row and stream are left as they
+// were; NULL when no task can overflow.
 template <int CAP>
-#ifndef TT_LS_WPE
-#define TT_LS_WPE 5
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE))) void local_search_kernel(DevProblem pb, uint8_t* __restrict__ slot,
-                                                          uint8_t* __restrict__ room, int64_t* __restrict__ rng,
-                                                          int P, int max_steps, double p1, double p2, double p3,
-                                                          uint8_t* __restrict__ redo_out,
-                                                          const uint8_t* __restrict__ redo_in,
-                                                          const int32_t* __restrict__ order) {
+__device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& pb, uint8_t* __restrict__ slot,
+                                                             uint8_t* __restrict__ room, int64_t* __restrict__ rng,
+                                                             long p, int max_steps, double p1, double p2, double p3,
+                                                             int32_t* __restrict__ redo_list) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int E = pb.E, R = pb.R, EW = pb.EW64;
     const int lane = threadIdx.x;
-    const long p = order ? (long)order[blockIdx.x] : (long)blockIdx.x;   // dispatch order only
-    if ((unsigned long)p >= (unsigned long)P) return;                     // not a permutation entry
-    if (redo_in && !redo_in[p]) return;
     LSP_T(t_kernel);
     const LsLayout L = ls_layout(E, R, EW, CAP);
     LsState S;
@@ -1191,7 +1185,74 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE)))
 #endif
     return;
 redo:
-    if (lane == 0) redo_out[p] = 1;
+    if (lane == 0) redo_list[2 + atomicAdd(&redo_list[0], 1)] = (int32_t)p;
+}
+
+#ifndef TT_LS_WPE
+#define TT_LS_WPE 5
+#endif
+// First launch: one wave per individual, in dispatch order `order` (NULL:
+// 0..P-1; entries outside 0..P-1 are skipped, tt_local_search_ordered checks
+// the permutation).
+template <int CAP>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE))) void local_search_kernel(
+    DevProblem pb, uint8_t* __restrict__ slot, uint8_t* __restrict__ room, int64_t* __restrict__ rng, int P,
+    int max_steps, double p1, double p2, double p3, int32_t* __restrict__ redo_list, const int32_t* __restrict__ order) {
+    const long p = order ? (long)order[blockIdx.x] : (long)blockIdx.x;   // dispatch order only
+    if ((unsigned long)p >= (unsigned long)P) return;
+    ls_one<CAP>(pb, slot, room, rng, p, max_steps, p1, p2, p3, redo_list);
+}
+
+// Redo launch: a grid of resident waves works through the individuals the
+// first launch listed, with full-size matcher tasks; the last wave to finish
+// resets the list for the stream's next call (no per-call memset). An empty
+// list costs one short launch.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE))) void local_search_redo_kernel(
+    DevProblem pb, uint8_t* __restrict__ slot, uint8_t* __restrict__ room, int64_t* __restrict__ rng, int max_steps,
+    double p1, double p2, double p3, int32_t* __restrict__ redo_list) {
+    const int n = redo_list[0];
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        __syncthreads();
+        ls_one<kMaxSlotEvents>(pb, slot, room, rng, (long)redo_list[2 + i], max_steps, p1, p2, p3, nullptr);
+    }
+    __threadfence();
+    if (threadIdx.x == 0 && atomicAdd(&redo_list[1], 1) == (int)gridDim.x - 1) {
+        redo_list[0] = 0;                                   // every wave has read the count
+        redo_list[1] = 0;
+    }
+}
+
+// Permutation check of a dispatch order (status bit 3 when it is not one):
+// every entry in 0..P-1, and the sum and the sum of squares (mod 2^64) equal
+// those of 0..P-1 -- a duplicate with a missing entry changes the sum.
+__global__ __launch_bounds__(1024) void order_check_kernel(const int32_t* __restrict__ order, int P,
+                                                           int32_t* __restrict__ status) {
+    __shared__ unsigned long long red[2][16];
+    __shared__ int bad_any;
+    if (threadIdx.x == 0) bad_any = 0;
+    __syncthreads();
+    unsigned long long s1 = 0, s2 = 0;
+    bool bad = false;
+    for (int i = threadIdx.x; i < P; i += 1024) {
+        const int v = order[i];
+        bad |= v < 0 || v >= P;
+        const unsigned long long d = (unsigned long long)(unsigned)v - (unsigned long long)(unsigned)i;
+        const unsigned long long q = (unsigned long long)(unsigned)v * (unsigned)v - (unsigned long long)(unsigned)i * (unsigned)i;
+        s1 += d;
+        s2 += q;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s1 += __shfl_down(s1, o);
+        s2 += __shfl_down(s2, o);
+    }
+    if (bad) atomicOr(&bad_any, 1);
+    if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = s1; red[1][threadIdx.x >> 6] = s2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long a = 0, b = 0;
+        for (int w = 0; w < 16; ++w) { a += red[0][w]; b += red[1][w]; }
+        if (bad_any || a || b) atomicOr(status, 8);
+    }
 }
 
 }  // namespace ttga
@@ -1226,24 +1287,43 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
     const LsLayout Lf = ls_layout(p->E, p->R, p->dev.EW64, kMaxSlotEvents);
     if (Lf.bytes > 160 * 1024) { set_error("instance too large for the local-search kernel"); return TT_ERR_LIMIT; }
     hipStream_t st = (hipStream_t)stream;
+    if (order) {
+        hipLaunchKernelGGL(order_check_kernel, dim3(1), dim3(1024), 0, st, order, P, p->dev.status);
+        TT_HIP(hipGetLastError());
+    }
     if (p->E <= kLsCapSmall) {                      // no slot can exceed the small tasks
         hipLaunchKernelGGL(local_search_kernel<kMaxSlotEvents>, dim3(P), dim3(64), Lf.bytes, st, p->dev, slot, room,
-                           rng, P, max_steps, p1, p2, p3, (uint8_t*)nullptr, (const uint8_t*)nullptr, order);
+                           rng, P, max_steps, p1, p2, p3, (int32_t*)nullptr, order);
         return check_hip(hipGetLastError(), "local_search launch");
     }
     const LsLayout Ls = ls_layout(p->E, p->R, p->dev.EW64, kLsCapSmall);
-    // per-call flags from the stream-ordered pool (hipMallocAsync reuses freed
-    // blocks; a buffer cached in the handle would race when one handle serves
-    // several streams, which the C-ABI allows)
-    uint8_t* redo = nullptr;
-    TT_HIP(hipMallocAsync((void**)&redo, (size_t)P, st));
-    TT_HIP(hipMemsetAsync(redo, 0, (size_t)P, st));
+    tt_problem* mp = const_cast<tt_problem*>(p);
+    std::lock_guard<std::mutex> lock(mp->ls_mu);
+    // this stream's redo list (grown stream-ordered: the old one may still be read)
+    tt_problem::LsRedo* rl = nullptr;
+    for (auto& r : mp->ls_redo)
+        if (r.stream == stream) rl = &r;
+    if (!rl) {
+        mp->ls_redo.push_back({stream, nullptr, 0});
+        rl = &mp->ls_redo.back();
+    }
+    if (rl->cap < P) {
+        if (rl->list) TT_HIP(hipFreeAsync(rl->list, st));
+        rl->list = nullptr;
+        rl->cap = 0;
+        TT_HIP(hipMallocAsync((void**)&rl->list, sizeof(int32_t) * ((size_t)P + 2), st));
+        TT_HIP(hipMemsetAsync(rl->list, 0, sizeof(int32_t) * 2, st));
+        rl->cap = P;
+    }
     hipLaunchKernelGGL(local_search_kernel<kLsCapSmall>, dim3(P), dim3(64), Ls.bytes, st, p->dev, slot, room, rng, P,
-                       max_steps, p1, p2, p3, redo, (const uint8_t*)nullptr, order);
+                       max_steps, p1, p2, p3, rl->list, order);
     TT_HIP(hipGetLastError());
-    hipLaunchKernelGGL(local_search_kernel<kMaxSlotEvents>, dim3(P), dim3(64), Lf.bytes, st, p->dev, slot, room, rng,
-                       P, max_steps, p1, p2, p3, (uint8_t*)nullptr, (const uint8_t*)redo, order);
+    // the redo launch: resident waves only (an empty list costs one short launch)
+    int per_cu = 0;
+    TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, local_search_redo_kernel, 64, Lf.bytes));
+    const int grid = std::min(P, std::max(1, per_cu) * p->num_cus);
+    hipLaunchKernelGGL(local_search_redo_kernel, dim3(grid), dim3(64), Lf.bytes, st, p->dev, slot, room, rng,
+                       max_steps, p1, p2, p3, rl->list);
     TT_HIP(hipGetLastError());
-    TT_HIP(hipFreeAsync(redo, st));
     return TT_OK;
 }

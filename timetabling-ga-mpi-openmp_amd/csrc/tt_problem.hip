@@ -242,6 +242,11 @@ int tt_problem_destroy(tt_problem* p) {
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(p->device);
+        if (!p->ls_redo.empty()) {                      // redo lists may be in use on their streams
+            (void)hipDeviceSynchronize();
+            for (auto& r : p->ls_redo) (void)hipFreeAsync(r.list, nullptr);
+            (void)hipDeviceSynchronize();
+        }
         rc = check_hip(hipFree(p->dev_block), "tt_problem_destroy");
         (void)hipSetDevice(prev);
     }

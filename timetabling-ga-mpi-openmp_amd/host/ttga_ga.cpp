@@ -462,13 +462,15 @@ struct Island {
     }
 
     // the reference thread whose replacement put pop[0] in place (ga.cpp:580-585):
-    // child c of the last tt_ga_replace (the sort key it leaves in `work`), else 0
+    // child c of the last tt_ga_replace (the source position it leaves at
+    // tt_ga_work_source_offset in `work`), else 0
     int best_thread(bool after_step) {
         if (!after_step) return 0;
-        uint64_t key = 0;
-        check_hip(hipMemcpyAsync(&key, work, 8, hipMemcpyDeviceToHost, st), "hipMemcpy");
+        int32_t s = 0;
+        check_hip(hipMemcpyAsync(&s, (const uint8_t*)work + tt_ga_work_source_offset(N, E), 4, hipMemcpyDeviceToHost,
+                                 st), "hipMemcpy");
         check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
-        const long src = (long)(key & 0xFFFFFFFFull), k = N - C;
+        const long src = s, k = N - C;
         return src >= k && src < N ? (int)(src - k) : 0;
     }
 

@@ -192,8 +192,9 @@ class Island(Members):
     def best_thread(self) -> int:
         """The reference thread (ga.cpp:498, one per child slot) whose
         replacement put the current pop[0] in place: child c of the last
-        tt_ga_replace (its sort key, include/ttga.h), else thread 0."""
-        src = int(self.work[:8].view(__import__("torch").int64)[0].item()) & 0xFFFFFFFF
+        tt_ga_replace (the source position it leaves in its own slot of the
+        work buffer, tt_ga_work_source_offset), else thread 0."""
+        src = self.dp.ga_work_source(self.work, self.N)
         k = self.N - self.C
         return src - k if self.generation > 0 and k <= src < self.N else 0
 

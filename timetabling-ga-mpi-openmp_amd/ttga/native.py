@@ -23,7 +23,7 @@ EXPORTS = (
     "tt_problem_create", "tt_problem_destroy", "tt_problem_dims", "tt_problem_derived", "tt_eval",
     "tt_eval_variant", "tt_assign_rooms", "tt_random_init", "tt_crossover", "tt_mutation", "tt_local_search",
     "tt_device_status", "tt_last_error", "tt_version", "tt_ga_breed", "tt_ga_work_bytes", "tt_ga_replace",
-    "tt_eval_auto_variant", "tt_local_search_ordered", "tt_lpt_order",
+    "tt_eval_auto_variant", "tt_local_search_ordered", "tt_lpt_order", "tt_ga_work_source_offset",
 )
 
 _lib = None
@@ -64,12 +64,14 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.tt_ga_breed.argtypes = [vp, vp, vp, vp, i32, vp, i32, dbl, dbl, i32, vp, vp, vp, vp]
     lib.tt_ga_work_bytes.argtypes = [i32, i32]
     lib.tt_ga_work_bytes.restype = ctypes.c_size_t
+    lib.tt_ga_work_source_offset.argtypes = [i32, i32]
+    lib.tt_ga_work_source_offset.restype = ctypes.c_size_t
     lib.tt_ga_replace.argtypes = [vp] * 7 + [i32] + [vp] * 6 + [i32, vp, vp]
     lib.tt_last_error.restype = ctypes.c_char_p
     lib.tt_last_error.argtypes = []
     lib.tt_version.argtypes = []
     for name in EXPORTS:
-        if name not in ("tt_last_error", "tt_ga_work_bytes"):
+        if name not in ("tt_last_error", "tt_ga_work_bytes", "tt_ga_work_source_offset"):
             getattr(lib, name).restype = ctypes.c_int
     if path is None:
         _lib = lib
@@ -231,6 +233,12 @@ class DeviceProblem:
         import torch
         return torch.empty(int(self.lib.tt_ga_work_bytes(N, self.E)), dtype=torch.uint8,
                            device=torch.device("cuda", self.device))
+
+    def ga_work_source(self, work, N) -> int:
+        """The merged position tt_ga_replace's new pop[0] came from (synchronises)."""
+        import torch
+        off = int(self.lib.tt_ga_work_source_offset(N, self.E))
+        return int(work[off:off + 4].view(torch.int32)[0].item())
 
     def ga_replace(self, pop, child, work):
         """pop/child: dicts of device tensors slot, room, hcv, scv, feasible, penalty."""

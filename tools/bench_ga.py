@@ -10,9 +10,17 @@ initial population is built and one warm-up generation).
 CPU: the reference's own per-child path of ga.cpp:543-577 (three
 RandomInitialSolution, two selection5, copies, crossover/copy, mutation,
 localSearch, computePenalty) on the host cores, OpenMP over children
-(oracle/_ref ref_ga_children_timed), on a sample of children bred from the
-same population. The reference's replace-worst + sort of its 10-member
-population is omitted from its timing (negligible there).
+(oracle/_ref ref_ga_children), on a sample of children bred from the
+population at the start of the timed generations, on the streams the device
+gives its first children of the next generation. The reference's replace-worst
++ sort of its 10-member population is omitted from its timing (negligible
+there).
+
+Bit-exactness: the same sample of children is bred, searched and evaluated on
+the device from the same population snapshot and streams (tt_ga_breed ->
+tt_local_search -> tt_eval) and compared with the reference's children:
+slots, rooms, hcv, scv, feasible, penalty and final RNG states
+("children_match_reference").
 
     python tools/bench_ga.py [--config comp01] [--pop 65536] [--children 65536]
                              [--gens 3] [--steps 200] [--cpu-sample 512]
@@ -24,7 +32,6 @@ are the GA's phase-2 regime (feasible parents, localSearch phase 2), where the
 reference spends most of a run.
 """
 import argparse
-import ctypes
 import json
 import os
 import pathlib
@@ -49,6 +56,8 @@ ap.add_argument("--config", default="comp01")
 ap.add_argument("--pop", type=int, default=65536)
 ap.add_argument("--children", type=int, default=65536)
 ap.add_argument("--gens", type=int, default=3)
+ap.add_argument("--min-seconds", type=float, default=0.0,
+                help="keep running timed generations until at least this much time has passed")
 ap.add_argument("--steps", type=int, default=200, help="maxSteps (-p 1: 200, -p 2: 1000, else 2000)")
 ap.add_argument("--seed", type=int, default=42)
 ap.add_argument("--cpu-sample", type=int, default=512)
@@ -75,38 +84,55 @@ while warm < a.warm_gens and float(isl.pop["feasible"].float().mean().item()) < 
     warm += 1
 feas_start = float(isl.pop["feasible"].float().mean().item())
 torch.cuda.synchronize()
-# snapshot of the population the CPU sample breeds from
+# snapshot of the population and child streams the CPU sample (and its device replay) breed from
 pop_slot, pop_room = isl.pop["slot"].cpu().numpy().copy(), isl.pop["room"].cpu().numpy().copy()
 pop_pen = isl.pop["penalty"].cpu().numpy().copy()
+snap = {k: v.clone() for k, v in isl.pop.items()}
+snap_rng = isl.rng_child.clone()
 t0 = time.perf_counter()
-for _ in range(a.gens):
+gens = 0
+while gens < a.gens or time.perf_counter() - t0 < a.min_seconds:
     isl.step()
+    gens += 1
+    if gens >= a.gens:
+        torch.cuda.synchronize()
 torch.cuda.synchronize()
 gpu_s = time.perf_counter() - t0
 feas, scv, hcv, pen = isl.member_meta(0)
+pf = isl.pop["feasible"].bool()
 out = {"config": a.config, "E": inst.E, "R": inst.R, "F": inst.F, "S": inst.S, "pop": a.pop,
-       "children_per_gen": a.children, "gens": a.gens, "max_steps": a.steps, "lpt_dispatch": isl.lpt,
+       "children_per_gen": a.children, "gens": gens, "max_steps": a.steps, "lpt_dispatch": isl.lpt,
        "init_seconds": init_s,
        "warm_gens": warm, "feasible_fraction_at_start": feas_start,
-       "gpu_seconds": gpu_s, "gpu_children_per_s": a.children * a.gens / gpu_s,
+       "gpu_seconds": gpu_s, "gpu_children_per_s": a.children * gens / gpu_s,
+       "best_scv_feasible": int(isl.pop["scv"][pf].min().item()) if bool(pf.any()) else None,
        "best": {"feasible": feas, "scv": scv, "hcv": hcv, "penalty": pen},
        "feasible_fraction": float(isl.pop["feasible"].float().mean().item())}
 
 from oracle_lib import ref  # noqa: E402
 R = ref()
 if R is not None and a.cpu_sample > 0:
-    n = a.cpu_sample
+    n = min(a.cpu_sample, a.children)
     threads, total, model = host_cores()
-    fn = R.lib.ref_ga_children_timed
-    fn.restype = ctypes.c_double
-    fn.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_void_p] + [ctypes.c_int] * 4
     h = R.problem(inst)
-    P_ = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-    pen32 = np.ascontiguousarray(pop_pen, dtype=np.int32)
+    seeds = snap_rng[:n].cpu().numpy().copy()
     res = {}
-    for as_is in (0, 1):
-        rng = ttga.population_seeds(777, n)
-        res[as_is] = fn(h.h, P_(pop_slot), P_(pop_room), P_(pen32), a.pop, P_(rng), n, a.steps, threads, as_is)
+    for as_is in (1, 0):       # as_is = 0 last: its children are the ones compared
+        ref_children, ref_rng, res[as_is] = h.ga_children(pop_slot, pop_room, pop_pen, seeds, a.steps, threads, as_is)
+    # the device replay of the same children from the snapshot
+    c = {k: torch.empty_like(v[:n]) for k, v in snap.items()}
+    g = torch.from_numpy(seeds).cuda()
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    dp.ga_breed(snap["slot"], snap["room"], snap["penalty"], g, c["slot"], c["room"], fl, isl.p_cross, isl.p_mut, True)
+    dp.local_search(c["slot"], c["room"], g, a.steps)
+    dp.eval(c["slot"], c["room"], out=(c["hcv"], c["scv"], c["feasible"], c["penalty"]))
+    torch.cuda.synchronize()
+    mism = [k for k in ("slot", "room", "hcv", "scv", "feasible", "penalty")
+            if not np.array_equal(c[k].cpu().numpy(), ref_children[k])]
+    if not np.array_equal(g.cpu().numpy(), ref_rng):
+        mism.append("rng")
+    out["children_match_reference"] = {"children": n, "match": not mism, "mismatched": mism,
+                                       "feasible_children": int(ref_children["feasible"].sum())}
     out["cpu_baseline"] = {"kind": "reference", "cores": threads, "cpu_model": model, "host_cores_total": total,
                            "sample_children": n, "seconds": res[0],
                            "children_per_s": n / res[0],

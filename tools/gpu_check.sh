@@ -27,7 +27,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py ;;
     benchsyn) run bench_syn 600 python -u bench.py --config syn --pop 262144 --steps 10 --warmup 2 ;;
-    profsyn) run rocprof_syn 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_syn" -o run --output-format csv -- python -u bench.py --config syn --pop 262144 --no-cpu --steps 10 --warmup 2 ;;
+    profsyn) run rocprof_syn 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_syn" -o run --output-format csv -- python -u bench.py --config syn --pop 262144 --no-pmc --no-cpu --steps 10 --warmup 2 ;;
     benchlg) run bench_lg 600 python -u bench.py --config lg --steps 100 ;;
     phases) run phases 300 python -u tools/eval_variants.py med 65536 8,24,40,72,136,264,520 ;;
     quality) run ga_quality 900 python -u tools/ga_quality.py --config sm --seeds 16 --gens 2001 --steps 200 --out "$OUT/ga_quality_sm.json" ;;

@@ -5,8 +5,15 @@ pass). Called BEFORE the parent touches the GPU; every pass runs under its own
 hard time limit, and any failure leaves the counters unmeasured (None).
 
 Per launch of the dominant kernel (median over its dispatches):
-  traffic   = FETCH_SIZE * 2 (gfx950 reports half the bytes of a wide
-              streaming read) + WRITE_SIZE, both in KiB -> bytes;
+  traffic   = FETCH_SIZE * k + WRITE_SIZE, both in KiB -> bytes, where the
+              read factor k is CALIBRATED in the same run: a fourth pass runs
+              the same kernel with its evaluation phases switched off
+              (tt_eval_variant profiling bits: only the population rows are
+              staged, exactly P*E bytes by the kernel's own load
+              instructions), k = P*E / FETCH_SIZE of that pass. The raw
+              FETCH_SIZE / WRITE_SIZE and k are reported next to the traffic
+              (MI355X_MICROARCH.md: FETCH_SIZE reads half the bytes of a wide
+              streaming read on gfx950; other widths are uncalibrated);
   lds_busy  = SQ_LDS_IDX_ACTIVE / (CUs * GRBM_GUI_ACTIVE / XCDs)  (LDS-array cycles)
   lds_conflict = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   valu_busy = 2 * SQ_INSTS_VALU / (4 * CUs * GRBM_GUI_ACTIVE / XCDs)  (wave64 VALU = 2 cycles on a SIMD32)
@@ -56,35 +63,64 @@ def _median_counters(root: str, kernel: str) -> dict:
     return dict(out)
 
 
-def collect(child_argv: list[str], kernel: str, timeout: int = 90) -> dict | None:
+def under_profiler() -> bool:
+    """True inside a rocprofv3 run (it exports ROCPROF* variables): the live
+    passes would start a profiler from a profiled, GPU-initialised process,
+    so the caller skips them."""
+    return any(k.startswith("ROCPROF") for k in os.environ)
+
+
+def _pass(prof, counters, child_argv, kernel, tmp, name, timeout):
+    d = os.path.join(tmp, name)
+    # the child gets this environment minus any profiler settings of our own
+    env = {k: v for k, v in os.environ.items() if not k.startswith("ROCPROF")}
+    env["TMPDIR"] = "/tmp"
+    cmd = ["timeout", "-s", "KILL", str(timeout), prof, "--pmc", *counters.split(), "--output-format", "csv",
+           "-d", d, "-o", "pmc", "--", sys.executable, *child_argv]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=timeout + 30)
+    except subprocess.TimeoutExpired:
+        return None
+    if r.returncode != 0:
+        sys.stderr.write(f"pmc pass {name} failed (rc {r.returncode}): {r.stderr[-500:]}\n")
+        return None
+    return _median_counters(d, kernel)
+
+
+def collect(child_argv: list[str], kernel: str, calib_argv: list[str] | None = None,
+            timeout: int = 90) -> dict | None:
     """Runs `python <child_argv>` once per pass under rocprofv3 --pmc and
-    returns the medians per launch of `kernel`, or None."""
+    returns the medians per launch of `kernel`, or None. calib_argv: the
+    calibration child (FETCH_SIZE only), whose values come back prefixed
+    CAL_."""
     prof = shutil.which("rocprofv3")
-    if prof is None:
+    if prof is None or under_profiler():
         return None
     out: dict = {}
-    env = dict(os.environ, TMPDIR="/tmp")
     with tempfile.TemporaryDirectory(prefix="ttga_pmc_", dir="/tmp") as tmp:
         for name, counters in PASSES.items():
-            d = os.path.join(tmp, name)
-            cmd = ["timeout", "-s", "KILL", str(timeout), prof, "--pmc", *counters.split(), "--output-format", "csv",
-                   "-d", d, "-o", "pmc", "--", sys.executable, *child_argv]
-            try:
-                r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=timeout + 30)
-            except subprocess.TimeoutExpired:
+            got = _pass(prof, counters, child_argv, kernel, tmp, name, timeout)
+            if got is None:
                 return None
-            if r.returncode != 0:
-                sys.stderr.write(f"pmc pass {name} failed (rc {r.returncode}): {r.stderr[-500:]}\n")
-                return None
-            out.update(_median_counters(d, kernel))
+            out.update(got)
+        if calib_argv:
+            got = _pass(prof, PASSES["fetch"], calib_argv, kernel, tmp, "calib", timeout)
+            if got:
+                out.update({"CAL_" + k: v for k, v in got.items()})
     return out
 
 
-def derive(c: dict | None) -> dict | None:
+def derive(c: dict | None, calib_bytes: float | None = None) -> dict | None:
+    """calib_bytes: the bytes the calibration launch reads (P*E)."""
     if not c or "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
         return None
-    res = {"traffic_bytes": (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0,
-           "fetch_kib": c["FETCH_SIZE"], "write_kib": c["WRITE_SIZE"]}
+    k, how = 2.0, "factor 2 from MI355X_MICROARCH.md (calibration pass missing)"
+    cal = c.get("CAL_FETCH_SIZE")
+    if calib_bytes and cal:
+        k, how = calib_bytes / (cal * 1024.0), "calibrated: population rows only, P*E bytes / FETCH_SIZE"
+    res = {"traffic_bytes": (k * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0,
+           "fetch_kib": c["FETCH_SIZE"], "write_kib": c["WRITE_SIZE"], "fetch_factor": k, "fetch_factor_how": how,
+           "calib_fetch_kib": cal, "calib_bytes": calib_bytes}
     g = c.get("GRBM_GUI_ACTIVE")
     if g:
         cyc = g / XCDS                                     # shader cycles of the launch (per XCD)
