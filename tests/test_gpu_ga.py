@@ -300,3 +300,30 @@ def test_local_search_order_permutation_check():
         dp.local_search(s, r, dev(seeds), 50, order=dev(order.astype(np.int32)))
         assert bool(dp.status() & 8) == bad, order[-3:]
         dp.close()
+
+
+def test_ga_trajectories_med_statistical():
+    """The north star's statistical GA comparison at a 400-event size (reduced
+    form of tools/ga_quality_program.py, whose full runs -- the reference
+    program itself, 16 seeds x 2001 generations -- are in
+    profiles/r03_ga_quality_{med,comp01}.json): the device GA (pop 10, one
+    child per generation, maxSteps 1000 as -p 2) against the reference's own
+    ga.cpp loop (oracle/_ref ref_ga_run, fresh crossover child) on the med
+    instance, 8 seeds x 500 generations: same feasibility count (Fisher) and
+    no detectable shift of the final best (Mann-Whitney U, p > 0.01)."""
+    from oracle_lib import host_threads, ref
+    R = ref()
+    if R is None:
+        pytest.skip("reference build oracle/_ref not present")
+    stats = pytest.importorskip("scipy.stats")
+    sys.path.insert(0, str(REPO / "tools"))
+    from ga_quality import device_runs
+    inst = ttga.config_instance("med")
+    seeds, gens, steps = list(range(1, 9)), 500, 1000
+    _, _, rfeas, _, rtrace, _ = R.problem(inst).ga_run(seeds, 10, gens, steps, 0, host_threads())
+    dfinal, dfeas, dtrace, _ = device_runs(inst, seeds, 10, gens, steps)
+    assert np.all(np.diff(dtrace, axis=1) <= 0)
+    table = [[int(dfeas.sum()), int(len(seeds) - dfeas.sum())], [int(rfeas.sum()), int(len(seeds) - rfeas.sum())]]
+    assert stats.fisher_exact(table)[1] > 0.01
+    p = stats.mannwhitneyu(dfinal, rtrace[:, -1], alternative="two-sided").pvalue
+    assert p > 0.01, (dfinal, rtrace[:, -1], p)

@@ -692,6 +692,55 @@ __device__ __forceinline__ void corr_chunk(const DevProblem& pb, int c, int lane
     }
 }
 
+// corr_chunk, software-pipelined (TT_CORR_SP): the B words of word w+1 for all
+// NB individuals are issued (volatile LDS loads: single ds_read_b64, never
+// paired into ds_read2_b64, in program order) before word w's popcounts, so
+// the compiler's lgkmcnt waits leave the next word's gathers in flight; the
+// correlation words stream from HBM/L2 four words ahead.
+#ifndef TT_CORR_SP
+#define TT_CORR_SP 1
+#endif
+template <int NB>
+__device__ __forceinline__ void corr_chunk_sp(const DevProblem& pb, int c, int lane, const uint32_t (&r)[NB],
+                                              int (&h)[NB]) {
+    typedef __attribute__((address_space(3))) volatile const uint64_t LdsWord;
+    const int E = pb.E, EW = pb.EW64, e = 64 * c + lane;
+    const bool ev = e < E;
+    const uint64_t* src = pb.cupT + (ev ? e : 0);
+    LdsWord* bp[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) bp[q] = (LdsWord*)(size_t)r[q];
+    uint64_t x0 = (ev && c < EW) ? src[(size_t)c * E] : 0ull;
+    uint64_t x1 = (ev && c + 1 < EW) ? src[(size_t)(c + 1) * E] : 0ull;
+    uint64_t x2 = (ev && c + 2 < EW) ? src[(size_t)(c + 2) * E] : 0ull;
+    uint64_t x3 = (ev && c + 3 < EW) ? src[(size_t)(c + 3) * E] : 0ull;
+    // ping-pong buffers a/b (no register rotation: a copy of an in-flight load
+    // would make the compiler wait for it at the copy)
+    uint64_t a[NB], b[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) a[q] = bp[q][c];
+    for (int w = c; w < EW; w += 2) {                              // wave-uniform
+        if (w + 1 < EW) {
+#pragma unroll
+            for (int q = 0; q < NB; ++q) b[q] = bp[q][w + 1];
+        }
+        asm volatile("" ::: "memory");                             // keep the gathers ahead of the popcounts
+        const uint64_t x4 = (ev && w + 4 < EW) ? src[(size_t)(w + 4) * E] : 0ull;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) h[q] = popc_acc(x0 & a[q], h[q]);
+        if (w + 1 >= EW) break;
+        if (w + 2 < EW) {
+#pragma unroll
+            for (int q = 0; q < NB; ++q) a[q] = bp[q][w + 2];
+        }
+        asm volatile("" ::: "memory");
+        const uint64_t x5 = (ev && w + 5 < EW) ? src[(size_t)(w + 5) * E] : 0ull;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) h[q] = popc_acc(x1 & b[q], h[q]);
+        x0 = x2; x1 = x3; x2 = x4; x3 = x5;
+    }
+}
+
 template <int NB, int MEPL>
 __global__ __launch_bounds__(1024) void eval_corr_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
                                                          const uint8_t* __restrict__ room, int P,
@@ -804,7 +853,11 @@ __global__ __launch_bounds__(1024) void eval_corr_kernel(DevProblem pb, const ui
                         const uint32_t sq = (q < nq && e < E) ? (uint32_t)lds[(size_t)q * WSI + L.off_sl + e] : 0u;
                         r[q] = lds0 + (q < nq ? q : 0) * WSI + sq * BSTB;
                     }
+#if TT_CORR_SP
+                    corr_chunk_sp<NB>(pb, c, lane, r, hq);
+#else
                     corr_chunk<NB>(pb, c, lane, r, hq);
+#endif
                 }
 #pragma unroll
                 for (int q = 0; q < NB; ++q) {

@@ -50,8 +50,16 @@ __device__ unsigned long long g_ls_prof[kPfN];
 #define LSP_CNT(St, i)
 #endif
 
+// TT_LS_SLP (default 1): slp[p] = slot of the event at scramble position p and
+// pos[e] = position of event e, kept with every accepted move, so a trial
+// window reads a partner's event and its slot in one LDS round trip instead
+// of two dependent ones.
+#ifndef TT_LS_SLP
+#define TT_LS_SLP 1
+#endif
+
 struct LsLayout {
-    size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, cnt, task;
+    size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, cnt, task, slp, pos;
     size_t task_bytes;
     int NT;              // events per matcher task (min(E, 256))
     size_t bytes;
@@ -66,6 +74,12 @@ __host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap) {
     L.rr = b; b += E;
     L.nrr = b; b += E;
     al(2); L.evl = b; b += 2 * (size_t)E;
+#if TT_LS_SLP
+    L.pos = b; b += 2 * (size_t)E;
+    L.slp = b; b += (size_t)E;
+#else
+    L.pos = L.slp = 0;
+#endif
     al(8); L.B = b; b += 8 * (size_t)kSlots * EW;
     L.NB = b; b += 8 * (size_t)kLsTasks * EW;
     L.rp = b; b += 4 * (size_t)kSlots;
@@ -97,6 +111,8 @@ struct LsState {
     int E, R, EW, lane;
     uint8_t *sl, *rr, *nrr;
     uint16_t* evl;
+    uint16_t* pos;       // [E] position of each event in evl (TT_LS_SLP)
+    uint8_t* slp;        // [E] slot of the event at each position (TT_LS_SLP)
     uint64_t *B, *NB;
     int32_t* rp;
     uint16_t* hist;
@@ -571,7 +587,12 @@ __device__ __forceinline__ void accept(LsState& S) {
             if (k < S.nts) S.rp[S.ts[k]] = S.misc[k];
 #pragma unroll
         for (int q = 0; q < 3; ++q)
-            if (q < S.nmv) S.sl[S.mv_e[q]] = (uint8_t)S.mv_t[q];
+            if (q < S.nmv) {
+                S.sl[S.mv_e[q]] = (uint8_t)S.mv_t[q];
+#if TT_LS_SLP
+                S.slp[S.pos[S.mv_e[q]]] = (uint8_t)S.mv_t[q];
+#endif
+            }
     }
     wave_sync();
     LSP_ADD(S, kPfSync, t0);
@@ -768,6 +789,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     S.pb = pb; S.E = E; S.R = R; S.EW = EW; S.lane = lane;
     S.sl = lds + L.sl; S.rr = lds + L.rr; S.nrr = lds + L.nrr;
     S.evl = (uint16_t*)(lds + L.evl);
+    S.pos = (uint16_t*)(lds + L.pos); S.slp = lds + L.slp;
     S.B = (uint64_t*)(lds + L.B); S.NB = (uint64_t*)(lds + L.NB);
     S.rp = (int32_t*)(lds + L.rp); S.hist = (uint16_t*)(lds + L.hist);
     S.misc = (int32_t*)(lds + L.misc);
@@ -824,17 +846,47 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
 
     LSP_T(t_scr);
     int64_t st = rng[p];
-    // scramble the event list (Solution.cpp:476-484): the stream is wave-uniform,
-    // lane 0 does the swaps, and the next draw overlaps the LDS round trip
-    for (int i = 0; i < E; ++i) {
-        const int j = pm_pick(st, E);
-        if (lane == 0) {
-            const uint16_t h = S.evl[i];
-            S.evl[i] = S.evl[j];
-            S.evl[j] = h;
+    // scramble the event list (Solution.cpp:476-484): swap i with a draw j_i for
+    // i = 0..E-1. The draws do not depend on the list, so they are taken 64 at a
+    // time, one per lane (lane k: state * 16807^(k+1), the Park-Miller jump; the
+    // first draws by Schrage, until an out-of-range seed is brought into range), and
+    // lane 0 then applies the block's swaps in order: only the LDS round trips of
+    // the swaps stay serial.
+    {
+        int i = 0;
+        // Schrage steps until the state is in range (one step, except for seeds >= 2^31)
+        for (; i < E && (i == 0 || (uint64_t)st >= kPmM); ++i) {
+            const int j = pm_pick(st, E);
+            if (lane == 0) {
+                const uint16_t h = S.evl[i];
+                S.evl[i] = S.evl[j];
+                S.evl[j] = h;
+            }
+        }
+        for (int i0 = i; i0 < E; i0 += 64) {
+            const int n = min(64, E - i0);
+            const uint32_t sk = pm_mulmod((uint32_t)st, jump);
+            const int jk = (int)__dmul_rn(__dmul_rn(1.0 / 2147483647.0, (double)sk), (double)E);
+            st = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)sk, n - 1);
+            for (int k = 0; k < n; ++k) {
+                const int j = __builtin_amdgcn_readlane(jk, k);
+                if (lane == 0) {
+                    const uint16_t h = S.evl[i0 + k];
+                    S.evl[i0 + k] = S.evl[j];
+                    S.evl[j] = h;
+                }
+            }
         }
     }
     __syncthreads();
+#if TT_LS_SLP
+    for (int q = lane; q < E; q += 64) {
+        const int e = S.evl[q];
+        S.pos[e] = (uint16_t)q;
+        S.slp[q] = S.sl[e];
+    }
+    __syncthreads();
+#endif
     LSP_ADD(S, kPfScramble, t_scr);
 
     LSP_ADD(S, kPfInit, t_kernel);
@@ -909,7 +961,14 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         // lb = corr_nb(ei) + corr_nb(ej) >= c = eah_i + eah_cur(ej)
                         const int rem = (i - j + E) % E;
                         // (ds_bpermute reads 0 from inactive lanes: every lane takes part)
+#if TT_LS_SLP
+                        int pk = j + lane;
+                        if (pk >= E) pk -= E;
+                        if (pk >= E) pk %= E;                      // E < 64 only
+                        const int ej = S.evl[pk], tj = S.slp[pk];
+#else
                         const int ej = S.evl[(j + lane) % E], tj = S.sl[ej];
+#endif
                         const int xt = bperm(V.x, tj);
                         bool need = true;
                         if (lane < rem && tj != t_orig) {
@@ -1072,7 +1131,14 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         // moved event in its new slot)
                         const int rem = (i - j + E) % E;
                         // (ds_bpermute reads 0 from inactive lanes: every lane takes part)
+#if TT_LS_SLP
+                        int pk = j + lane;
+                        if (pk >= E) pk -= E;
+                        if (pk >= E) pk %= E;                      // E < 64 only
+                        const int ej = S.evl[pk], tj = S.slp[pk];
+#else
                         const int ej = S.evl[(j + lane) % E], tj = S.sl[ej];
+#endif
                         const uint64_t rw = bperm64(V.row, ej >> 6), zw = bperm64(V.z, ej >> 6);
                         const int xt = bperm(V.x, tj);
                         bool need = true;
