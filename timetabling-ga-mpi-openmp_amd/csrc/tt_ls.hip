@@ -50,12 +50,13 @@ __device__ unsigned long long g_ls_prof[kPfN];
 #define LSP_CNT(St, i)
 #endif
 
-// TT_LS_SLP (default 1): slp[p] = slot of the event at scramble position p and
+// TT_LS_SLP (default 0): slp[p] = slot of the event at scramble position p and
 // pos[e] = position of event e, kept with every accepted move, so a trial
 // window reads a partner's event and its slot in one LDS round trip instead
-// of two dependent ones.
+// of two dependent ones. Same-box A/B (profiles/r03_s2_ab.json): +6 % on the
+// comp01 local search (phase 1 and 2), -2 % on med phase 2; off.
 #ifndef TT_LS_SLP
-#define TT_LS_SLP 1
+#define TT_LS_SLP 0
 #endif
 
 struct LsLayout {
