@@ -88,8 +88,18 @@ __device__ __forceinline__ uint32_t pm_pow(int n) {
 // (int)(next() * n): truncation of the fp64 product (Solution.cpp:52, ga.cpp:135)
 __device__ __forceinline__ int pm_pick(int64_t& s, int n) { return (int)__dmul_rn(pm_next(s), (double)n); }
 
-// Full-wave sum (every lane active): DPP row shifts + readlane, no LDS round trips.
-__device__ __forceinline__ int wave_sum(int v) { return __reduce_add_sync(~0ull, v); }
+// Full-wave sum (every lane active): DPP row shifts + readlane, no LDS round
+// trips. Written out rather than __reduce_add_sync, whose library reduction
+// also carries a partial-EXEC path at every call site (code size: the local
+// search inlines it dozens of times).
+__device__ __forceinline__ int wave_sum(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x101, 0xf, 0xf, true);    // row_shl:1 (lane i += lane i+1)
+    v += __builtin_amdgcn_update_dpp(0, v, 0x102, 0xf, 0xf, true);    // row_shl:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x104, 0xf, 0xf, true);    // row_shl:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x108, 0xf, 0xf, true);    // row_shl:8: lane 16r holds row r's sum
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+           __builtin_amdgcn_readlane(v, 48);
+}
 
 // Index of this thread's wave in the workgroup, as a wave-uniform (SGPR) value
 // so that loops and loads driven by it stay scalar.

@@ -312,105 +312,6 @@ __device__ __forceinline__ int lane_scv_runs(const uint8_t* my, const DevProblem
     return sc;
 }
 
-// ---------------------------------------------------------------- student runs, vector-memory records
-// The wide path's lane phase streams the whole record set (125 KB at syn) through
-// every tile, so its records miss the scalar cache; a record load on the LGKM
-// counter is then waited for by the step's own LDS waits. Here the records come
-// by buffer loads (VM counter, wave-uniform offsets, two steps ahead) into VGPRs,
-// and each id is taken by the address add itself (v_add_u32_sdwa WORD_0/WORD_1).
-#ifndef TT_LANES_VM
-#define TT_LANES_VM 0
-#endif
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-template <int NQ>
-struct RecRegs {
-    u32x4v q[NQ];
-};
-// vz: a zero the compiler cannot prove wave-uniform, so the loaded records stay
-// in VGPRs instead of being moved to SGPRs by a readfirstlane that waits for
-// the load.
-template <int NQ>
-__device__ __forceinline__ void rec_load(RecRegs<NQ>& r, __amdgpu_buffer_rsrc_t rs, int vz, int byte_off) {
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) r.q[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, vz, byte_off + 16 * k, 0);
-}
-// K students of N ids from the dwords of r
-template <int N, int K, int NQ>
-__device__ __forceinline__ int students_scv_vm(const uint8_t* my, const RecRegs<NQ>& r) {
-    constexpr int H = N / 2;
-    uint32_t sl[K * N];
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            const int d = k * H + (j >> 1);
-            const uint32_t w = r.q[d >> 2][d & 3];
-            sl[k * N + j] = my[(j & 1) ? (w >> 16) : (w & 0xFFFFu)];
-        }
-    int sc = 0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        uint64_t m = 0;
-#pragma unroll
-        for (int j = 0; j < N; ++j) m |= 1ull << (sl[k * N + j] & 63);
-        sc += mask_scv(m);
-    }
-    return sc;
-}
-// A run of cnt students of N ids from dword off: K students per step, the
-// records of step i + 2 requested while step i is evaluated (three register
-// sets used in rotation: no copy of an in-flight load).
-template <int N>
-__device__ __forceinline__ int run_scv_vm(const uint8_t* my, __amdgpu_buffer_rsrc_t rs, int vz, int off, int cnt) {
-    constexpr int K = N <= 16 ? 2 : 1;
-    constexpr int ST = K * N / 2;                  // dwords per step
-    constexpr int NQ = (ST + 3) / 4;
-    const int steps = cnt / K;
-    const int b0 = 4 * off;
-    int sc = 0;
-    if (steps > 0) {
-        RecRegs<NQ> a, b, c;
-        auto boff = [&](int i) { return b0 + 4 * ST * (i < steps ? i : steps - 1); };
-        rec_load(a, rs, vz, boff(0));
-        rec_load(b, rs, vz, boff(1));
-        for (int i = 0; i < steps; i += 3) {
-            rec_load(c, rs, vz, boff(i + 2));
-            sc += students_scv_vm<N, K>(my, a);
-            if (i + 1 >= steps) break;
-            rec_load(a, rs, vz, boff(i + 3));
-            sc += students_scv_vm<N, K>(my, b);
-            if (i + 2 >= steps) break;
-            rec_load(b, rs, vz, boff(i + 4));
-            sc += students_scv_vm<N, K>(my, c);
-        }
-    }
-    if constexpr (K == 2) {
-        if (cnt & 1) {
-            RecRegs<(N / 2 + 3) / 4> r;
-            rec_load(r, rs, vz, b0 + 4 * ST * steps);
-            sc += students_scv_vm<N, 1>(my, r);
-        }
-    }
-    return sc;
-}
-__device__ __forceinline__ int lane_scv_runs_vm(const uint8_t* my, const DevProblem& pb, int r0, int r1) {
-    const ConstI32* runs = (const ConstI32*)pb.srun;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)pb.sid, 0, 0x7FFFFFFF, 0x00020000);
-    const int vz = (pb.E >> 20) * (int)threadIdx.x;          // 0 (E < 2^20), but lane-dependent to the compiler
-    int sc = 0;
-    for (int k = r0; k < r1; ++k) {
-        const int n = runs[4 * k], off = runs[4 * k + 1], cnt = runs[4 * k + 2];
-        switch (n) {
-#define TT_RUN(N) case N: sc += run_scv_vm<N>(my, rs, vz, off, cnt); break;
-            TT_RUN(2) TT_RUN(4) TT_RUN(6) TT_RUN(8) TT_RUN(10) TT_RUN(12) TT_RUN(14) TT_RUN(16)
-            TT_RUN(18) TT_RUN(20) TT_RUN(22) TT_RUN(24) TT_RUN(26) TT_RUN(28) TT_RUN(30) TT_RUN(32)
-#undef TT_RUN
-            default: sc += run_scv_any(my, (const ConstU32*)(pb.sid + off), cnt, n); break;
-        }
-    }
-    return sc;
-}
-
 // Phase ablations (tt_eval_variant's profiling bits) are compiled in only with
 // -DTT_EVAL_ABLATE=1: as runtime flags they put a uniform branch around every
 // per-event atomic, which also serialises each cell-counter return.
@@ -711,11 +612,7 @@ __global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, con
         }
         if (threadIdx.x < 64) tile[threadIdx.x * SP + E] = 63;
         __syncthreads();
-#if TT_LANES_VM
-        const int sc = r0 < r1 ? lane_scv_runs_vm(tile + lane * SP, pb, r0, r1) : 0;
-#else
         const int sc = r0 < r1 ? lane_scv_runs<2>(tile + lane * SP, pb, r0, r1) : 0;
-#endif
         part[wv * 64 + lane] = sc;
         __syncthreads();
         if (wv == 0 && lane < np) {

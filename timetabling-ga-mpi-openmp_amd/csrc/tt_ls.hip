@@ -39,12 +39,14 @@ constexpr int kLsCapSmall = 64;
 // Profiling build (-DTT_LS_PROF, `make libttga_prof.so`, tools/ls_prof.py):
 // per-section shader-clock totals of every wave, summed into g_ls_prof.
 #ifdef TT_LS_PROF
-enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfQ1, kPfQ1c, kPfQ1m, kPfQ2, kPfQ2c, kPfQ2m, kPfP1m2, kPfP1m2lb, kPfP1m1m, kPfP1m1a, kPfP1m1k, kPfMaxTotal, kPfN };
+enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfQ1, kPfQ1c, kPfQ1m, kPfQ2, kPfQ2c, kPfQ2m, kPfP1m2, kPfP1m2lb, kPfP1m1m, kPfP1m1a, kPfP1m1k, kPfVis1, kPfM1p1, kPfM2p1, kPfPh1, kPfPh2, kPfVis2, kPfM1p2, kPfM2p2, kPfMaxTotal, kPfN };
 __device__ unsigned long long g_ls_prof[kPfN];
 #define LSP_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define LSP_ADD(St, i, v) ((St).prof[i] += __builtin_amdgcn_s_memtime() - (v))
 #define LSP_CNT(St, i) ((St).prof[i] += 1)
+#define LSP_SET(v) ((v) = __builtin_amdgcn_s_memtime())
 #else
+#define LSP_SET(v)
 #define LSP_T(v)
 #define LSP_ADD(St, i, v)
 #define LSP_CNT(St, i)
@@ -363,6 +365,35 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
     LSP_ADD(S, kPfMatch, t0);
 }
 
+// Lane-serial matcher for a touched slot of 64 < N <= 256 events (one lane):
+// rare, so out of line (TT_LS_SERIAL_CALL) -- inlined at each of match_tasks'
+// call sites it made up much of the kernel's 166 KB of code. Returns the
+// slot's room-clash pairs; the rooms go to nrr.
+#ifndef TT_LS_TASK_LOOP
+#define TT_LS_TASK_LOOP 1
+#endif
+#ifndef TT_LS_SERIAL_CALL
+#define TT_LS_SERIAL_CALL 1
+#endif
+#if TT_LS_SERIAL_CALL
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+int match_task_serial(int R, int N, const uint64_t* poss, uint16_t* ev, uint64_t* pl, uint8_t* mr, uint8_t* rm,
+                      uint8_t* dr, uint16_t* hist, uint8_t* nrr) {
+    for (int i = 0; i < N; ++i) pl[i] = poss[ev[i]];
+    for (int r = 0; r < R; ++r) hist[r] = 0;
+    match_slot<4>(R, ev, pl, N, mr, rm, dr, nrr);
+    int pairs = 0;
+    for (int i = 0; i < N; ++i) {
+        const int r = nrr[ev[i]];
+        pairs += hist[r];
+        hist[r] = (uint16_t)(hist[r] + 1);
+    }
+    return pairs;
+}
+
 // Builds NB[k] for the touched slots; lane k lists the events of slot k.
 __device__ __forceinline__ void build_nb(LsState& S) {
     LSP_T(t0);
@@ -447,14 +478,19 @@ __device__ __forceinline__ bool match_tasks(LsState& S, int kmask, const TaskReg
     if (S.c1_valid && S.nts == 2) kmask &= ~2;
     if (!(kmask & ((1 << S.nts) - 1))) return false;            // nothing to match: no sync
     LSP_T(t0);
-    const int* tn = tr.tn;
-    const int* tev = tr.tev;
-    const uint64_t* tpl = tr.tpl;
+    // TT_LS_TASK_LOOP: the task loop stays a loop (one inlined matcher per call
+    // site instead of three); the task's registers are picked by selects
+#if TT_LS_TASK_LOOP
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
     for (int k = 0; k < 3; ++k) {
         if (k >= S.nts) break;
         if (!((kmask >> k) & 1)) continue;
-        const int N = tn[k];
+        const int N = k == 0 ? tr.tn[0] : k == 1 ? tr.tn[1] : tr.tn[2];
+        const int tevk = k == 0 ? tr.tev[0] : k == 1 ? tr.tev[1] : tr.tev[2];
+        const uint64_t tplk = k == 0 ? tr.tpl[0] : k == 1 ? tr.tpl[1] : tr.tpl[2];
         if (N > S.NT) {                                             // task capacity exceeded
             if (S.lane == 0) {
                 if (S.NT < kMaxSlotEvents && S.NT < S.E) {
@@ -471,20 +507,11 @@ __device__ __forceinline__ bool match_tasks(LsState& S, int kmask, const TaskReg
         } else if (N == 0) {
             if (S.lane == 0) S.misc[k] = 0;
         } else if (N <= 64) {
-            match_task_wave(S, k, N, tev[k], tpl[k]);
+            match_task_wave(S, k, N, tevk, tplk);
         } else {                                                    // 64 < N <= 256: lane-serial matcher
             if (S.lane == 0) {
                 const LsTask T = get_task(S, k);
-                for (int i = 0; i < N; ++i) T.pl[i] = S.pb.poss[T.ev[i]];
-                for (int r = 0; r < S.R; ++r) T.hist[r] = 0;
-                match_slot<4>(S.R, T.ev, T.pl, N, T.mr, T.rm, T.dr, S.nrr);
-                int pairs = 0;
-                for (int i = 0; i < N; ++i) {
-                    const int r = S.nrr[T.ev[i]];
-                    pairs += T.hist[r];
-                    T.hist[r] = (uint16_t)(T.hist[r] + 1);
-                }
-                S.misc[k] = pairs;
+                S.misc[k] = match_task_serial(S.R, N, S.pb.poss, T.ev, T.pl, T.mr, T.rm, T.dr, T.hist, S.nrr);
             }
             wave_sync();
         }
@@ -785,6 +812,9 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     const int E = pb.E, R = pb.R, EW = pb.EW64;
     const int lane = threadIdx.x;
     LSP_T(t_kernel);
+#ifdef TT_LS_PROF
+    uint64_t t_ph = 0;                  // phase timer (assigned, not declared, between the gotos and redo:)
+#endif
     const LsLayout L = ls_layout(E, R, EW, CAP);
     LsState S;
     S.pb = pb; S.E = E; S.R = R; S.EW = EW; S.lane = lane;
@@ -901,12 +931,14 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     const long guard_max = 4l * (long)E * ((long)max_steps + 2) + 1024;
     long guard = 0;
     const bool fast1 = EW <= 64;                                        // row words fit the lanes
+    LSP_SET(t_ph);
     if (!feasible_now(S)) {                                             // phase 1 (Solution.cpp:497-618)
         for (int i = 0; evc < E; i = (i + 1) % E) {
             if (step > max_steps || ++guard > guard_max) break;
             const int ei = S.evl[i];
             LSP_CNT(S, kPfVisits);
-            if (ehcv_cur(S, ei) == 0) { evc++; continue; }
+            LSP_T(t_vis);
+            if (ehcv_cur(S, ei) == 0) { evc++; LSP_ADD(S, kPfVis1, t_vis); continue; }
             const int t_orig = S.sl[ei];
             Visit2 V;
             if (fast1) visit2_row_x(S, ei, V);
@@ -914,6 +946,8 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
             // accepted, and every acceptance leaves this event's loops
             const int eah_i = fast1 ? S.rp[t_orig] + __builtin_amdgcn_readlane(V.x, t_orig) - (int)row_bit(V.row, ei)
                                     : eah_cur(S, ei);
+            LSP_ADD(S, kPfVis1, t_vis);
+            LSP_T(t_m1);
             const int t_start = pm_pick(st, kSlots);
             for (int h = 0, t = t_start; h < kSlots; t = (t + 1) % kSlots, h++) {
                 if (step > max_steps) break;
@@ -946,8 +980,10 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                 }
             }
             cache_drop(S);
+            LSP_ADD(S, kPfM1p1, t_m1);
             if (better) { better = false; continue; }
             if (p2 != 0) {
+                LSP_T(t_m2);
                 // B[t_orig] without ei: the partner's slot-mates after a swap
                 uint64_t bo = 0;
                 if (fast1 && lane < EW) {
@@ -1021,6 +1057,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                     if (acc) { evc = 0; better = true; break; }
                     j = (j + 1) % E;
                 }
+                LSP_ADD(S, kPfM2p1, t_m2);
                 if (better) { better = false; continue; }
             }
             if (p3 != 0) {
@@ -1056,6 +1093,8 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
             evc++;
         }
     }
+    LSP_ADD(S, kPfPh1, t_ph);
+    LSP_SET(t_ph);
     if (feasible_now(S)) {                                              // phase 2 (Solution.cpp:619-768)
         // owner table in place of the room histogram (rooms are distinct per slot now)
         S.phase2 = 1;
@@ -1069,12 +1108,15 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
             if (step > max_steps || ++guard > guard_max) break;
             const int ei = S.evl[i];
             LSP_CNT(S, kPfVisits);
+            LSP_T(t_vis);
             int cur, scs_i;
             scv_terms(S, ei, false, cur, scs_i);
-            if (cur == 0) { evc++; continue; }
+            if (cur == 0) { evc++; LSP_ADD(S, kPfVis2, t_vis); continue; }
             const int ti = S.sl[ei];
             Visit2 V;
             if (fast) visit2_row_x(S, ei, V);
+            LSP_ADD(S, kPfVis2, t_vis);
+            LSP_T(t_m1);
             const int t_start = pm_pick(st, kSlots);
             for (int h = 0; h < kSlots;) {
                 if (step > max_steps) break;
@@ -1121,8 +1163,10 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                 restore_task<0>(S);
             }
             cache_drop(S);
+            LSP_ADD(S, kPfM1p2, t_m1);
             if (better) { better = false; continue; }
             if (p2 != 0) {
+                LSP_T(t_m2);
                 if (fast) visit2_z(S, ei, V);
                 int j = (i + 1) % E;
                 while (j != i) {
@@ -1197,6 +1241,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                     if (acc) { evc = 0; better = true; break; }
                     j = (j + 1) % E;
                 }
+                LSP_ADD(S, kPfM2p2, t_m2);
                 if (better) { better = false; continue; }
             }
             if (p3 != 0) {
@@ -1233,6 +1278,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
             evc++;
         }
     }
+    LSP_ADD(S, kPfPh2, t_ph);
     if (guard > guard_max && lane == 0) atomicOr(pb.status, 4);
 
     __syncthreads();
