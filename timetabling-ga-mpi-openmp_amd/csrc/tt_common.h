@@ -101,6 +101,12 @@ __device__ __forceinline__ int wave_sum(int v) {
            __builtin_amdgcn_readlane(v, 48);
 }
 
+// Wave ballot / any of a bool: the builtin takes the compare's lane mask as
+// it is (HIP's __ballot(int) first turns the bool into 0/1 in a VGPR and
+// compares it again: two more VALU per ballot).
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0ull; }
+
 // Index of this thread's wave in the workgroup, as a wave-uniform (SGPR) value
 // so that loops and loads driven by it stay scalar.
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }

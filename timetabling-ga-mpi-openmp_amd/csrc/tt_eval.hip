@@ -312,9 +312,11 @@ __device__ __forceinline__ int lane_scv_runs(const uint8_t* my, const DevProblem
     return sc;
 }
 
-// Phase ablations (tt_eval_variant's profiling bits) are compiled in only with
-// -DTT_EVAL_ABLATE=1: as runtime flags they put a uniform branch around every
-// per-event atomic, which also serialises each cell-counter return.
+// Per-event phase ablations (tt_eval_variant's profiling bits 4..32) are compiled
+// in only with -DTT_EVAL_ABLATE=1: as runtime flags they put a uniform branch
+// around every per-event atomic, which also serialises each cell-counter
+// return. Bits 1 and 2 (skip the lane / wave phase: once per tile or batch)
+// stay, for bench.py's FETCH_SIZE calibration pass (staging and outputs only).
 #ifndef TT_EVAL_ABLATE
 #define TT_EVAL_ABLATE 0
 #endif
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
                                                               uint8_t* __restrict__ feas_out,
                                                               int32_t* __restrict__ pen_out, int ablate_arg) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int ablate = TT_EVAL_ABLATE ? ablate_arg : 0;
+    const int ablate = TT_EVAL_ABLATE ? ablate_arg : (ablate_arg & 3);   // phase skips: once per tile / batch
     constexpr int NT = 64 * NW;
     const int E = pb.E, R = pb.R;
     const int lane = threadIdx.x & 63, wv = wave_id();
@@ -489,7 +491,7 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
             uint32_t smax = 0, rmax = 0;
 #pragma unroll
             for (int r = 0; r < EWC; ++r) { smax = max(smax, sv[r]); rmax = max(rmax, rv[r]); }
-            const bool any_bad = __any(smax >= (uint32_t)kSlots || rmax >= (uint32_t)R);
+            const bool any_bad = wave_any(smax >= (uint32_t)kSlots || rmax >= (uint32_t)R);
             int h = 0, last = 0;
             if (!any_bad) {
                 if (!(ablate & 32))
@@ -781,7 +783,7 @@ __global__ __launch_bounds__(1024) void eval_corr_kernel(DevProblem pb, const ui
                                                          uint8_t* __restrict__ feas_out, int32_t* __restrict__ pen_out,
                                                          int ablate_arg) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int ablate = TT_EVAL_ABLATE ? ablate_arg : 0;
+    const int ablate = TT_EVAL_ABLATE ? ablate_arg : (ablate_arg & 3);   // phase skips: once per tile / batch
     const int E = pb.E, R = pb.R, EW = pb.EW64;
     const CorrLayout L = corr_layout(E, R, EW, NB);
     const int lane = threadIdx.x & 63, wv = wave_id();
@@ -864,7 +866,7 @@ __global__ __launch_bounds__(1024) void eval_corr_kernel(DevProblem pb, const ui
                 // per-lane partials (conflict-free, no return); summed once per batch
                 atomicAdd(&red[(2 * q) * 64 + lane], h);
                 atomicAdd(&red[(2 * q + 1) * 64 + lane], last);
-                if (__any(bad) && lane == 0) atomicOr(&acc[4 * q + 2], 1);
+                if (wave_any(bad) && lane == 0) atomicOr(&acc[4 * q + 2], 1);
             }
         }
         __syncthreads();

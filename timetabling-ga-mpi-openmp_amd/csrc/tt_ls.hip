@@ -30,11 +30,6 @@ constexpr int kLsTasks = 3;
 // input by the second launch with tasks sized for kMaxSlotEvents.
 constexpr int kLsCapSmall = 64;
 
-// ballots per block of the wave matcher's room transpose (4: fewer wasted
-// ballots past R; same results, A/B in tools/ab_ls.py)
-#ifndef TT_LS_TRU
-#define TT_LS_TRU 4
-#endif
 
 // Profiling build (-DTT_LS_PROF, `make libttga_prof.so`, tools/ls_prof.py):
 // per-section shader-clock totals of every wave, summed into g_ls_prof.
@@ -240,6 +235,26 @@ __device__ __forceinline__ void scv_terms(LsState& S, int e, bool nb, int& es, i
     LSP_ADD(S, kPfScv, t0);
 }
 
+// TT_LS_WLT: the matcher's room transpose by v_writelane instead of a
+// compare-and-select per room.
+#ifndef TT_LS_WLT
+#define TT_LS_WLT 1
+#endif
+// lane j of (lo, hi) = the 64-bit wave-uniform v. The lane select goes
+// through M0 (gfx9 reads one SGPR per VALU instruction besides M0); the s_nop
+// pads the M0 write (inline asm gets no hazard padding from the compiler).
+// Nothing else in the local-search kernel uses M0 (no LDS-DMA, no movrel), so
+// clobbering it is safe; clang warns that M0 is reserved.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void writelane64(uint32_t& lo, uint32_t& hi, uint64_t v, int j) {
+    asm volatile("s_mov_b32 m0, %4\n\ts_nop 1\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
+                 : "+v"(lo), "+v"(hi)
+                 : "s"((uint32_t)v), "s"((uint32_t)(v >> 32)), "s"(j)
+                 : "m0");
+}
+#pragma clang diagnostic pop
+
 // Wave matcher for one touched slot of N <= 64 events, the same search as
 // match_slot<1> (tt_match.h, Solution.cpp:772-891), with its state in
 // registers: lane i holds event i's possible-room mask (pl) and matched room
@@ -261,16 +276,27 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
     constexpr uint32_t NONE = 0xFFu;
     const bool act = lane < N;
     const uint32_t pl_lo = (uint32_t)pl, pl_hi = (uint32_t)(pl >> 32);
-    // transpose: ev_of_room (lane j) = the events whose possible rooms include j
-    // (TT_LS_TRU independent ballots per block; pl has no bits at or above R)
+    // transpose: ev_of_room (lane j) = the events whose possible rooms include j:
+    // one ballot per room, written into lane j by v_writelane; pl is zero past the
+    // N events (load_tasks)
+#if TT_LS_WLT
+    uint32_t eor_lo = 0, eor_hi = 0;
+    {
+        const int r1 = R < 32 ? R : 32;
+        for (int j = 0; j < r1; ++j) writelane64(eor_lo, eor_hi, ballot((pl_lo >> j) & 1u), j);
+        for (int j = 32; j < R; ++j) writelane64(eor_lo, eor_hi, ballot((pl_hi >> (j - 32)) & 1u), j);
+    }
+    const uint64_t eor = ((uint64_t)eor_hi << 32) | eor_lo;
+#else
     uint64_t eor = 0;
-    for (int j0 = 0; j0 < R; j0 += TT_LS_TRU) {
+    for (int j0 = 0; j0 < R; j0 += 4) {
 #pragma unroll
-        for (int q = 0; q < TT_LS_TRU; ++q) {
-            const uint64_t b = __ballot((pl >> (j0 + q)) & 1ull);   // pl is zero past the N events (load_tasks)
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t b = ballot((pl >> (j0 + q)) & 1ull);
             if (lane == j0 + q) eor = b;
         }
     }
+#endif
     // lane j also keeps the possible rooms of its matched event (plr), so a
     // search step reads rm and plr at the same lane j: no dependent readlane
     uint32_t mr = NONE, rm = 0, dr = 0, plr_lo = 0, plr_hi = 0;
@@ -279,7 +305,7 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
     for (;;) {
         // stage 1 (closed form): expand all unmatched events, ascending
         const uint64_t cand = eor & unm;
-        uint64_t sr = __ballot(lane < R && cand != 0ull), fr = sr;
+        uint64_t sr = ballot(lane < R && cand != 0ull), fr = sr;
         if (cand) dr = (uint32_t)__builtin_ctzll(cand);
         // stage 2: fringe rooms ascending; a matched room's event is expanded at
         // once. Each room enters the fringe once and each matched event is
@@ -295,7 +321,7 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
             const uint64_t freef = fr & ~rmatched;
             const uint64_t M = fr & (freef ? (freef & (0ull - freef)) - 1ull : ~0ull);
             const uint64_t plr = ((uint64_t)plr_hi << 32) | plr_lo;
-            const uint64_t disc = __ballot(((M >> lane) & 1ull) && (plr & ~sr) != 0ull);
+            const uint64_t disc = ballot(((M >> lane) & 1ull) && (plr & ~sr) != 0ull);
             LSP_CNT(S, kPfMatchSteps);
             if (!disc) {                                   // the walk reaches the lowest free room
                 if (freef) sink = __builtin_ctzll(freef);
@@ -330,7 +356,7 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
     // free possible room, else the first possible room; one with no possible room
     // keeps lessBusy carried over from the previous unplaced event (initially 0)
     const bool un = act && mr == NONE;
-    const uint64_t unb = __ballot(un);
+    const uint64_t unb = ballot(un);
     uint32_t r = mr;
     if (unb) {                                     // wave-uniform: usually every event is placed
         uint32_t v = 0;
@@ -341,7 +367,7 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
                 if (fr2) v = (uint32_t)__builtin_ctzll(fr2);
             }
         }
-        const uint64_t carriers = __ballot(un && pl != 0ull);
+        const uint64_t carriers = ballot(un && pl != 0ull);
         const uint64_t below = carriers & ((1ull << lane) - 1ull);
         const int src = below ? 63 - __builtin_clzll(below) : lane;
         const uint32_t carried = (uint32_t)__shfl((int)v, src, 64);
@@ -371,6 +397,13 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
 // slot's room-clash pairs; the rooms go to nrr.
 #ifndef TT_LS_TASK_LOOP
 #define TT_LS_TASK_LOOP 1
+#endif
+#ifndef TT_LS_M1WIN
+#define TT_LS_M1WIN 1
+#endif
+// visit rows one visit ahead: same-box A/B +2..+11 % (profiles/r03_s5_ab.json); off
+#ifndef TT_LS_ROWPF
+#define TT_LS_ROWPF 0
 #endif
 #ifndef TT_LS_SERIAL_CALL
 #define TT_LS_SERIAL_CALL 1
@@ -713,6 +746,23 @@ __device__ __forceinline__ void visit2_row_x(LsState& S, int ei, Visit2& V) {
     V.x = x;
 }
 
+// the same from the visited event's row already in registers (lane w: word w)
+__device__ __forceinline__ void visit2_x_from_row(LsState& S, uint64_t row, Visit2& V) {
+    const int EW = S.EW, lane = S.lane;
+    V.row = row;
+    int x = 0;
+    for (int w = 0; w < EW; ++w) {
+        const uint64_t rw = readlane64(row, w);
+        if (lane < kSlots) x += __popcll(rw & S.B[(size_t)lane * EW + w]);
+    }
+    V.x = x;
+}
+
+// corr64 row of event e, one word per lane (lanes < EW), for the next visit
+__device__ __forceinline__ uint64_t load_row(const LsState& S, int e) {
+    return S.lane < S.EW ? S.pb.corr64[(size_t)e * S.EW + S.lane] : 0ull;
+}
+
 __device__ __forceinline__ void visit2_z(LsState& S, int ei, Visit2& V) {
     const int EW = S.EW, lane = S.lane, ti = S.sl[ei];
     uint64_t z = 0;
@@ -742,7 +792,7 @@ __device__ __forceinline__ bool matchable(LsState& S, int s, int out, int a) {
     const int o = lane < R ? (int)S.hist[s * R + lane] : 0xFFFF;
     const bool valid = o != 0xFFFF && o != out;
     const uint64_t po = valid ? S.pb.poss[o] : 0ull;
-    const uint64_t used = __ballot(valid);
+    const uint64_t used = ballot(valid);
     const uint64_t fre = (R >= 64 ? ~0ull : ((1ull << R) - 1)) & ~used;
     uint64_t seen = S.pb.poss[a];
     if (seen & fre) return true;
@@ -782,12 +832,12 @@ __device__ __forceinline__ int window_resolve(int lane, uint32_t jump, int64_t& 
     const uint32_t sk = pm_mulmod((uint32_t)st, jump);
     const bool valid = lane < rem;
     const bool d = valid && __dmul_rn(1.0 / 2147483647.0, (double)sk) < p;
-    const uint64_t dm = __ballot(d);
+    const uint64_t dm = ballot(d);
     const uint64_t lt = (1ull << lane) - 1ull;
     const bool alive = valid && step + __popcll(dm & lt) <= max_steps;
-    const uint64_t am = __ballot(alive);
+    const uint64_t am = ballot(alive);
     const int kend = am == ~0ull ? 64 : __builtin_ctzll(~am);
-    const uint64_t nm = __ballot(alive && d && need);
+    const uint64_t nm = ballot(alive && d && need);
     const int kstar = nm ? __builtin_ctzll(nm) : 64;
     const int last = kstar < 64 ? kstar : kend - 1;                    // last trial drawn
     if (last >= 0) {
@@ -850,7 +900,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     for (int c = lane; c < kSlots * EW; c += 64) S.B[c] = 0ull;
     for (int c = lane; c < kSlots * R; c += 64) S.hist[c] = 0;
     __syncthreads();
-    if (__any(bad)) {                       // invalid genome: leave it untouched
+    if (wave_any(bad)) {                       // invalid genome: leave it untouched
         if (lane == 0) atomicOr(pb.status, 2);
         return;
     }
@@ -933,15 +983,25 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     const bool fast1 = EW <= 64;                                        // row words fit the lanes
     LSP_SET(t_ph);
     if (!feasible_now(S)) {                                             // phase 1 (Solution.cpp:497-618)
+        // TT_LS_ROWPF: the visited event's correlation row loaded one visit ahead
+        // (the scrambled event list is fixed, so the next visit's event is known)
+        uint64_t nrow = (fast1 && TT_LS_ROWPF) ? load_row(S, S.evl[0]) : 0ull;
         for (int i = 0; evc < E; i = (i + 1) % E) {
             if (step > max_steps || ++guard > guard_max) break;
             const int ei = S.evl[i];
             LSP_CNT(S, kPfVisits);
             LSP_T(t_vis);
-            if (ehcv_cur(S, ei) == 0) { evc++; LSP_ADD(S, kPfVis1, t_vis); continue; }
+            uint64_t row = nrow;
+            if (fast1 && TT_LS_ROWPF) nrow = load_row(S, S.evl[i + 1 < E ? i + 1 : 0]);
+            else if (fast1) row = load_row(S, ei);
+            // eventHcv(ei) (Solution.cpp:173-191)
+            const int ehcv = fast1 ? (int)S.hist[S.sl[ei] * R + S.rr[ei]] - 1 +
+                                         row_in_set(S, row, S.B + (size_t)S.sl[ei] * EW) - (int)row_bit(row, ei)
+                                   : ehcv_cur(S, ei);
+            if (ehcv == 0) { evc++; LSP_ADD(S, kPfVis1, t_vis); continue; }
             const int t_orig = S.sl[ei];
             Visit2 V;
-            if (fast1) visit2_row_x(S, ei, V);
+            if (fast1) visit2_x_from_row(S, row, V);
             // eventAffectedHcv(ei) in the current state: unchanged until a trial is
             // accepted, and every acceptance leaves this event's loops
             const int eah_i = fast1 ? S.rp[t_orig] + __builtin_amdgcn_readlane(V.x, t_orig) - (int)row_bit(V.row, ei)
@@ -949,10 +1009,28 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
             LSP_ADD(S, kPfVis1, t_vis);
             LSP_T(t_m1);
             const int t_start = pm_pick(st, kSlots);
-            for (int h = 0, t = t_start; h < kSlots; t = (t + 1) % kSlots, h++) {
+            for (int h = 0; h < kSlots;) {
                 if (step > max_steps) break;
-                if (pm_next(st) < p1) {
+                if (TT_LS_M1WIN && fast1 && S.c1_valid && (uint64_t)st < kPmM) {
+                    // window: lane k screens target t_start+h+k against the kept task's
+                    // bound X[t] + misc[1] >= c (the scalar test below is the same). Only
+                    // with the old-slot task kept: before that the first trial runs anyway
+                    const int rem = kSlots - h;
+                    const int tk = (t_start + h + lane) % kSlots;
+                    const int xt = bperm(V.x, tk);                          // every lane takes part
+                    const bool skip = tk != t_orig && xt + S.misc[1] >= eah_i + S.rp[tk];
+                    const bool need = lane < rem && !skip;
+                    bool done;
+                    const int ks = window_resolve(lane, jump, st, step, max_steps, rem, p1, need, done);
+                    if (ks == 64) break;                                // rem <= 45 < 64: the loop ends here
+                    h += ks;
+                } else {
+                    if (!(pm_next(st) < p1)) { h++; continue; }
                     step++;
+                }
+                const int t = (t_start + h) % kSlots;
+                h++;
+                {
                     const int c = eah_i + S.rp[t];
                     // the kept old-slot task gives misc[1]; corr_nb(ei) in t is X[t]
                     if (fast1 && S.c1_valid && t != t_orig && __builtin_amdgcn_readlane(V.x, t) + S.misc[1] >= c) continue;
@@ -1104,17 +1182,21 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
         wave_sync();
         const bool fast = fast1;
         evc = 0;
+        uint64_t nrow = (fast && TT_LS_ROWPF) ? load_row(S, S.evl[0]) : 0ull;
         for (int i = 0; evc < E; i = (i + 1) % E) {
             if (step > max_steps || ++guard > guard_max) break;
             const int ei = S.evl[i];
             LSP_CNT(S, kPfVisits);
             LSP_T(t_vis);
+            uint64_t row = nrow;
+            if (fast && TT_LS_ROWPF) nrow = load_row(S, S.evl[i + 1 < E ? i + 1 : 0]);
+            else if (fast) row = load_row(S, ei);
             int cur, scs_i;
             scv_terms(S, ei, false, cur, scs_i);
             if (cur == 0) { evc++; LSP_ADD(S, kPfVis2, t_vis); continue; }
             const int ti = S.sl[ei];
             Visit2 V;
-            if (fast) visit2_row_x(S, ei, V);
+            if (fast) visit2_x_from_row(S, row, V);
             LSP_ADD(S, kPfVis2, t_vis);
             LSP_T(t_m1);
             const int t_start = pm_pick(st, kSlots);
