@@ -35,6 +35,13 @@ typedef __attribute__((address_space(4))) const uint32_t ConstU32;
 typedef __attribute__((address_space(4))) const int32_t ConstI32;
 
 // ---------------------------------------------------------------- eval_tile5
+// TT_T5_ROOMBUF: slot-row DMA and room rows by buffer instructions (per-tile
+// resource, 32-bit lane offsets): no 64-bit per-lane pointer lives across the
+// tile loop (it spilled to scratch: 8 B per thread per tile, 4 MB per launch at
+// P = 65,536).
+#ifndef TT_T5_ROOMBUF
+#define TT_T5_ROOMBUF 1
+#endif
 // NW waves per 64-individual tile; one tile per workgroup (the loop also runs a
 // persistent grid). Slot rows are staged by LDS-DMA (DB: two tile buffers, the
 // next tile of a persistent grid lands under the current one's evaluation).
@@ -359,9 +366,23 @@ __host__ __device__ inline Tile5Layout tile5_layout(int E, int R, int NW, bool D
 // One wave's share of a tile's slot rows by LDS-DMA (global_load_lds_dword:
 // 64 lanes x 4 B land contiguously at a wave-uniform LDS address, so a row of
 // E/4 <= 112 dwords takes two instructions and keeps its padded stride SP).
+// Buffer-load form (TT_T5_ROOMBUF): a per-tile resource, a 32-bit lane offset
+// and a scalar row offset (the global form kept a 64-bit per-lane pointer live
+// across the tile loop, which spilled to scratch).
 template <int NW>
 __device__ __forceinline__ void tile_dma(const uint8_t* src, uint8_t* dst, int np, int E, int SP, int wv, int lane) {
     const int qd = E >> 2;
+#if TT_T5_ROOMBUF
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, np * E, 0x00020000);
+    for (int r = wv; r < np; r += NW) {
+        if (lane < qd)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + r * SP), 4,
+                                                     4 * lane, r * E, 0, 0);
+        if (lane + 64 < qd)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + r * SP + 256),
+                                                     4, 4 * lane + 256, r * E, 0, 0);
+    }
+#else
     for (int r = wv; r < np; r += NW) {
         const uint32_t* g = (const uint32_t*)(src + (long)r * E);
         auto* d = (__attribute__((address_space(3))) void*)(dst + r * SP);
@@ -371,6 +392,7 @@ __device__ __forceinline__ void tile_dma(const uint8_t* src, uint8_t* dst, int n
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + 64 + lane),
                                              (__attribute__((address_space(3))) void*)(dst + r * SP + 256), 4, 0, 0);
     }
+#endif
 }
 
 template <int EWC, int NW, int PK, bool DB = false>
@@ -465,18 +487,37 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
         }
 
         // ---- lane phase (lane = individual): attendance masks of this wave's students
-        const int sc = (!(ablate & 1) && r0 < r1) ? lane_scv_runs<1>(tile + lane * SP, pb, r0, r1) : 0;
+        // lane * SP recomputed per tile (an asm multiply the compiler cannot hoist:
+        // kept live across the tile loop, the product spilled to scratch)
+        uint32_t lsp;
+        asm volatile("v_mul_u32_u24 %0, %1, %2" : "=v"(lsp) : "v"(lane), "s"(SP));
+        const int sc = (!(ablate & 1) && r0 < r1) ? lane_scv_runs<1>(tile + lsp, pb, r0, r1) : 0;
         part[wv * 64 + lane] = sc;
 
         // ---- wave phase (wave = individual): hcv terms + last-slot term
         const int nq = (ablate & 2) ? 0 : np;
         uint32_t pfn[EWC];                                        // room row, one individual ahead
+#if TT_T5_ROOMBUF
+        // room rows by buffer loads from a per-tile resource: a 32-bit lane offset
+        // and a scalar row offset instead of a 64-bit per-lane pointer kept live
+        // across the tile loop (it spilled to scratch: 8 B per thread per tile)
+        const __amdgpu_buffer_rsrc_t rrs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(room + p0 * E), 0, 64 * E, 0x00020000);
+        auto load_row = [&](const uint8_t*, int q, uint32_t* dst) {
+#pragma unroll
+            for (int r = 0; r < EWC; ++r)
+                dst[r] = (!last_partial || r < EWC - 1 || lane + 64 * r < E)
+                             ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rrs, lane + 64 * r, q * E, 0)
+                             : 0u;
+        };
+#else
         auto load_row = [&](const uint8_t* base, int q, uint32_t* dst) {
             const uint8_t* rr = base + (p0 + q) * E;
 #pragma unroll
             for (int r = 0; r < EWC; ++r)
                 dst[r] = (!last_partial || r < EWC - 1 || lane + 64 * r < E) ? rr[lane + 64 * r] : 0u;
         };
+#endif
         if (wv < nq) load_row(room, wv, pfn);
         for (int q = wv; q < nq; q += NW) {
             uint32_t rv[EWC], sv[EWC];
