@@ -60,18 +60,31 @@ def test_breed_vs_oracle(sm, N, C, skip):
     assert (fl & 1).any() and (fl & 2).any() if C >= 10 else True
 
 
-# N up to 65,536: the tiled sort (8,192-key LDS tiles + global steps above them)
-@pytest.mark.parametrize("N,C", [(10, 1), (10, 4), (300, 300), (5000, 100), (20000, 3000), (65536, 8192)])
-def test_replace_vs_oracle(sm, N, C):
+# N up to 65,536: the tiled sort (8,192-key LDS tiles + global steps above them) for
+# C > 8,192; for C <= 8,192 the merge of the survivors with the sorted children
+# when the survivors are in order (presorted: as a previous tt_ga_replace leaves
+# them; "migrant": one survivor out of order, as after a migration), else the
+# one-workgroup fallback sort
+@pytest.mark.parametrize("N,C,order", [(10, 1, "random"), (10, 4, "random"), (300, 300, "random"),
+                                       (5000, 100, "random"), (20000, 3000, "random"), (65536, 8192, "random"),
+                                       (20000, 9000, "random"), (10, 4, "presorted"), (300, 300, "presorted"),
+                                       (5000, 100, "presorted"), (65536, 8192, "presorted"),
+                                       (65536, 8192, "migrant"), (4096, 1, "migrant")])
+def test_replace_vs_oracle(sm, N, C, order):
     inst, dp, o = sm
     rng = np.random.default_rng(N + C)
     def rand_pop(n):
         pen = rng.integers(0, 40, n).astype(np.int32)       # many ties: checks the stable order
+        pen[rng.integers(0, n, max(1, n // 50))] = -1        # invalid genomes sort last
         return dict(slot=rng.integers(0, 45, (n, inst.E), dtype=np.uint8),
                     room=rng.integers(0, inst.R, (n, inst.E), dtype=np.uint8),
                     hcv=rng.integers(0, 9, n).astype(np.int32), scv=rng.integers(0, 99, n).astype(np.int32),
                     feasible=rng.integers(0, 2, n).astype(np.uint8), penalty=pen)
     pop, ch = rand_pop(N), rand_pop(C)
+    if order != "random":
+        pop["penalty"] = np.sort(pop["penalty"].astype(np.uint32)).astype(np.int32)   # key order: -1 last
+        if order == "migrant":
+            pop["penalty"][(N - C) // 2] = 39 + 1              # one survivor out of order
     exp = o.ga_replace(pop, ch)
     gpop = {k: dev(v) for k, v in pop.items()}
     dp.ga_replace(gpop, {k: dev(v) for k, v in ch.items()}, dp.ga_work(N))

@@ -171,6 +171,83 @@ __global__ void bitonic_step_kernel(uint64_t* __restrict__ keys, int NP, int k, 
     }
 }
 
+// ---- merge form of the sort (TT_GA_MERGE): the survivors (positions < k = N-C)
+// of a population that a previous tt_ga_replace left sorted are already in key
+// order, so the sorted merged population is the merge of them with the C
+// children's keys sorted on their own (one workgroup in LDS for C <= kSortTile).
+// Keys are unique (positions), so the merge equals the full sort. The survivors'
+// order is checked on the device; when it does not hold (the first call after
+// initialisation, a migration generation) a one-workgroup full sort runs instead.
+#ifndef TT_GA_MERGE
+#define TT_GA_MERGE 1
+#endif
+
+__device__ __forceinline__ void lds_bitonic(uint64_t* sk, int NP) {
+    for (int k = 2; k <= NP; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int q = threadIdx.x; q < NP / 2; q += blockDim.x) {
+                const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1)), l = i + j;
+                const uint64_t x = sk[i], y = sk[l];
+                if ((x > y) == ((i & k) == 0)) { sk[i] = y; sk[l] = x; }
+            }
+            __syncthreads();
+        }
+}
+
+// flag[0] = 1 when the survivors are in key order; ckeys = the children's keys sorted
+__global__ __launch_bounds__(1024) void replace_prep_kernel(const int32_t* __restrict__ pen,
+                                                            const int32_t* __restrict__ cpen, int N, int C, int CP,
+                                                            uint64_t* __restrict__ ckeys, int32_t* __restrict__ flag) {
+    __shared__ uint64_t sk[kSortTile];
+    __shared__ int bad;
+    const int k = N - C;
+    if (threadIdx.x == 0) bad = 0;
+    for (int i = threadIdx.x; i < CP; i += blockDim.x) sk[i] = i < C ? sort_key(cpen[i], k + i) : ~0ull;
+    __syncthreads();
+    bool b = false;
+    for (int i = threadIdx.x; i + 1 < k; i += blockDim.x) b |= (uint32_t)pen[i] > (uint32_t)pen[i + 1];
+    if (b) bad = 1;                                       // benign race: any writer stores 1
+    lds_bitonic(sk, CP);
+    for (int i = threadIdx.x; i < C; i += blockDim.x) ckeys[i] = sk[i];
+    if (threadIdx.x == 0) flag[0] = bad ? 0 : 1;
+}
+
+// merge path: output i takes the i-th smallest of survivors (pen[a], a) and ckeys
+__global__ void replace_merge_kernel(const int32_t* __restrict__ pen, int N, int C, const uint64_t* __restrict__ ckeys,
+                                     const int32_t* __restrict__ flag, uint64_t* __restrict__ mkeys) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N || flag[0] == 0) return;
+    const int k = N - C;
+    int lo = max(0, i - C), hi = min(i, k);
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sort_key(pen[mid], mid) < ckeys[i - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+    }
+    const int a = lo, b = i - a;
+    const uint64_t ka = a < k ? sort_key(pen[a], a) : ~0ull, kb = b < C ? ckeys[b] : ~0ull;
+    mkeys[i] = ka < kb ? ka : kb;
+}
+
+// the fallback: full bitonic sort of keys[0..NP) by one workgroup in global memory
+// (keys, 8 B each, stay L2-resident); nothing to do when the merge ran
+__global__ __launch_bounds__(1024) void replace_fallback_sort_kernel(uint64_t* __restrict__ keys, int NP,
+                                                                     const int32_t* __restrict__ flag,
+                                                                     uint64_t* __restrict__ mkeys, int N) {
+    if (flag[0] != 0) return;
+    for (int k = 2; k <= NP; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int q = threadIdx.x; q < NP / 2; q += blockDim.x) {
+                const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1)), l = i + j;
+                const uint64_t x = keys[i], y = keys[l];
+                if ((x > y) == ((i & k) == 0)) { keys[i] = y; keys[l] = x; }
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+    for (int i = threadIdx.x; i < N; i += blockDim.x) mkeys[i] = keys[i];
+}
+
 // gather the sorted population into the work rows (one wave per row)
 __global__ __launch_bounds__(64) void replace_gather_kernel(int E, int N, int C, const uint64_t* __restrict__ keys,
                                                             const uint8_t* __restrict__ ps, const uint8_t* __restrict__ pr,
@@ -295,15 +372,17 @@ extern "C" int tt_ga_breed(const tt_problem* p, const uint8_t* pop_slot, const u
 }
 
 // work layout: sort keys [pow2(N)] u64 | slot rows [N][E] | room rows [N][E] |
-// meta [N][4] i32 | the source slot (256 B, written only by tt_ga_replace)
+// meta [N][4] i32 | the source slot (256 B, written only by tt_ga_replace) |
+// merged keys [N] u64 | sorted child keys [kSortTile] u64 | merge flag (256 B)
 static size_t work_source_offset(int N, int E) {
     const size_t NP = (size_t)pow2_at_least(N);
     return align256(8 * NP) + 2 * align256((size_t)N * E) + align256(16 * (size_t)N);
 }
+static size_t work_merge_offset(int N, int E) { return work_source_offset(N, E) + 256; }
 
 extern "C" size_t tt_ga_work_bytes(int N, int E) {
     if (N < 1 || E < 1) return 0;
-    return work_source_offset(N, E) + 256;
+    return work_merge_offset(N, E) + align256(8 * (size_t)N) + 8 * (size_t)kSortTile + 256;
 }
 
 extern "C" size_t tt_ga_work_source_offset(int N, int E) {
@@ -333,8 +412,22 @@ extern "C" int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* po
     int32_t* wm = (int32_t*)(wr + align256((size_t)N * E));
     hipLaunchKernelGGL(replace_keys_kernel, dim3((NP + 255) / 256), dim3(256), 0, st, pop_penalty, child_penalty, N, C,
                        NP, keys);
-    sort_keys(keys, NP, st);
-    hipLaunchKernelGGL(replace_gather_kernel, dim3(N), dim3(64), 0, st, E, N, C, keys, pop_slot, pop_room, pop_hcv,
+    const uint64_t* sorted = keys;
+    if (TT_GA_MERGE && C <= kSortTile) {
+        uint64_t* mkeys = (uint64_t*)(w + work_merge_offset(N, E));
+        uint64_t* ckeys = (uint64_t*)((uint8_t*)mkeys + align256(8 * (size_t)N));
+        int32_t* flag = (int32_t*)(ckeys + kSortTile);
+        const int CP = pow2_at_least(std::max(C, 2));
+        hipLaunchKernelGGL(replace_prep_kernel, dim3(1), dim3(1024), 0, st, pop_penalty, child_penalty, N, C, CP, ckeys,
+                           flag);
+        hipLaunchKernelGGL(replace_merge_kernel, dim3((N + 255) / 256), dim3(256), 0, st, pop_penalty, N, C, ckeys, flag,
+                           mkeys);
+        hipLaunchKernelGGL(replace_fallback_sort_kernel, dim3(1), dim3(1024), 0, st, keys, NP, flag, mkeys, N);
+        sorted = mkeys;
+    } else {
+        sort_keys(keys, NP, st);
+    }
+    hipLaunchKernelGGL(replace_gather_kernel, dim3(N), dim3(64), 0, st, E, N, C, sorted, pop_slot, pop_room, pop_hcv,
                        pop_scv, pop_feasible, pop_penalty, child_slot, child_room, child_hcv, child_scv, child_feasible,
                        child_penalty, ws, wr, wm, (int32_t*)(w + work_source_offset(N, E)));
     hipLaunchKernelGGL(replace_scatter_kernel, dim3(N), dim3(64), 0, st, E, ws, wr, wm, pop_slot, pop_room, pop_hcv,

@@ -21,6 +21,10 @@ namespace ttga {
 
 constexpr uint8_t kNone = 0xFF;
 
+#ifndef TT_BUCKETS_CHUNK
+#define TT_BUCKETS_CHUNK 1
+#endif
+
 // Per-wave LDS scratch for one individual.
 struct MatchScratch {
     uint8_t* sl;        // [E]     slot of each event
@@ -33,6 +37,7 @@ struct MatchScratch {
     int32_t* bstart;    // [46]    bucket offsets
     uint32_t* tmp;      // [64]
     uint32_t* flags;    // [4]
+    uint64_t* cm;       // [64]    per-slot lane masks of one 64-event chunk (build_buckets)
 };
 
 __host__ __device__ inline size_t match_scratch_bytes(int E, int R) {
@@ -47,6 +52,8 @@ __host__ __device__ inline size_t match_scratch_bytes(int E, int R) {
     b += 2 * (size_t)kSlots * R;             // rm, dr
     b = (b + 3) & ~(size_t)3;
     b += 4 * 46 + 4 * 64 + 4 * 4;            // bstart, tmp, flags
+    b = (b + 7) & ~(size_t)7;
+    b += 8 * 64;                             // cm
     return (b + 15) & ~(size_t)15;
 }
 
@@ -65,7 +72,9 @@ __device__ inline MatchScratch carve_match_scratch(uint8_t* base, int E, int R) 
     b = (b + 3) & ~(size_t)3;
     m.bstart = (int32_t*)(base + b); b += 4 * 46;
     m.tmp = (uint32_t*)(base + b); b += 4 * 64;
-    m.flags = (uint32_t*)(base + b);
+    m.flags = (uint32_t*)(base + b); b += 4 * 4;
+    b = (b + 7) & ~(size_t)7;
+    m.cm = (uint64_t*)(base + b);
     return m;
 }
 
@@ -95,6 +104,28 @@ __device__ inline void build_buckets(const DevProblem& pb, MatchScratch& m, int 
     const int start = incl - c;
     if (lane < kSlots) m.bstart[lane] = start;
     if (lane == kSlots - 1) m.bstart[kSlots] = incl;
+#if TT_BUCKETS_CHUNK
+    // stable fill, 64 events at a time: each event sets its lane bit in its slot's
+    // chunk mask; its place is the slot's running count plus the lower lanes of the
+    // mask (ascending event order inside a bucket, as the lane walk below)
+    m.cm[lane] = 0ull;
+    int cur = start;                                  // lane t < 45: slot t's next position
+    __syncthreads();
+    for (int c0 = 0; c0 < E; c0 += 64) {
+        const int e = c0 + lane;
+        const int s = e < E ? m.sl[e] : 0xFF;
+        if (s < kSlots) atomicOr((unsigned long long*)&m.cm[s], 1ull << lane);
+        const int base = __shfl(cur, s < kSlots ? s : 0, 64);       // every lane takes part
+        __syncthreads();
+        if (s < kSlots) m.bev[base + __popcll(m.cm[s] & ((1ull << lane) - 1ull))] = (uint16_t)e;
+        __syncthreads();
+        if (lane < kSlots) {
+            cur += __popcll(m.cm[lane]);
+            m.cm[lane] = 0ull;
+        }
+        __syncthreads();
+    }
+#else
     // stable fill: lane t walks the slot row (broadcast reads) and keeps its events
     int pos = start;
     int e = 0;
@@ -108,6 +139,7 @@ __device__ inline void build_buckets(const DevProblem& pb, MatchScratch& m, int 
     }
     for (; e < E; ++e)
         if (m.sl[e] == me) m.bev[pos++] = (uint16_t)e;
+#endif
     __syncthreads();
     const int nb = m.bstart[kSlots];
     for (int b = lane; b < nb; b += 64) m.pl[b] = pb.poss[m.bev[b]];

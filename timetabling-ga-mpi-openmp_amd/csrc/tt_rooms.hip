@@ -9,6 +9,9 @@
 namespace ttga {
 
 constexpr int kMaxRejections = 1 << 20;
+#ifndef TT_ROOMS_ABL
+#define TT_ROOMS_ABL 0
+#endif
 
 // ---------------------------------------------------------------- helpers
 __device__ inline void load_row(uint8_t* dst, const uint8_t* src, int E, int lane) {
@@ -32,7 +35,9 @@ __global__ __launch_bounds__(64) void assign_rooms_kernel(DevProblem pb, const u
     for (int e = lane; e < E; e += 64) m.rr[e] = 0xFF;   // events with an invalid slot stay 255
     __syncthreads();
     build_buckets(pb, m, lane);
+#if TT_ROOMS_ABL != 1                                    // profiling builds only: buckets alone
     assign_touched(pb, m, ~0ull, lane);
+#endif
     store_row(room + p * E, m.rr, E, lane);
 }
 
