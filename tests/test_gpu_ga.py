@@ -185,10 +185,11 @@ def test_native_driver_matches_python_driver(tmp_path, sm):
 
 def test_lpt_order_vs_numpy(sm):
     """tt_lpt_order: indices by key descending, ties by index, negative keys last
-    (the sizes cover the one-workgroup sort and the tiled one)."""
+    (the sizes cover the small LDS sort, the register-blocked one-workgroup sort
+    up to 8,192 keys -- in-thread, in-wave and cross-wave steps -- and the tiled one)."""
     inst, dp, o = sm
     rng = np.random.default_rng(8)
-    for n in (1, 100, 4096, 5000, 20000):
+    for n in (1, 5, 8, 9, 100, 511, 512, 513, 4096, 5000, 8192, 20000):
         key = rng.integers(-1, 30, n).astype(np.int32)
         hi = np.where(key < 0, np.int64(2 ** 32), np.int64(2 ** 31 - 1) - key.astype(np.int64))
         exp = np.lexsort((np.arange(n), hi)).astype(np.int32)

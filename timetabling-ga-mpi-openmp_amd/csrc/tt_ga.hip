@@ -182,41 +182,31 @@ __global__ void bitonic_step_kernel(uint64_t* __restrict__ keys, int NP, int k, 
 #define TT_GA_MERGE 1
 #endif
 
-__device__ __forceinline__ void lds_bitonic(uint64_t* sk, int NP) {
-    for (int k = 2; k <= NP; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int q = threadIdx.x; q < NP / 2; q += blockDim.x) {
-                const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1)), l = i + j;
-                const uint64_t x = sk[i], y = sk[l];
-                if ((x > y) == ((i & k) == 0)) { sk[i] = y; sk[l] = x; }
-            }
-            __syncthreads();
-        }
-}
-
-// flag[0] = 1 when the survivors are in key order; ckeys = the children's keys sorted
-__global__ __launch_bounds__(1024) void replace_prep_kernel(const int32_t* __restrict__ pen,
-                                                            const int32_t* __restrict__ cpen, int N, int C, int CP,
-                                                            uint64_t* __restrict__ ckeys, int32_t* __restrict__ flag) {
-    __shared__ uint64_t sk[kSortTile];
-    __shared__ int bad;
+// kPrepBlocks workgroups: flag[g] = 1 when workgroup g's share of the survivors
+// is in key order (all of them together: the survivors are); ckeys = the
+// children's keys (padded to CP), sorted by the next launch
+constexpr int kPrepBlocks = 64;
+__global__ __launch_bounds__(256) void replace_prep_kernel(const int32_t* __restrict__ pen,
+                                                           const int32_t* __restrict__ cpen, int N, int C, int CP,
+                                                           uint64_t* __restrict__ ckeys, int32_t* __restrict__ flag) {
     const int k = N - C;
-    if (threadIdx.x == 0) bad = 0;
-    for (int i = threadIdx.x; i < CP; i += blockDim.x) sk[i] = i < C ? sort_key(cpen[i], k + i) : ~0ull;
-    __syncthreads();
-    bool b = false;
-    for (int i = threadIdx.x; i + 1 < k; i += blockDim.x) b |= (uint32_t)pen[i] > (uint32_t)pen[i + 1];
-    if (b) bad = 1;                                       // benign race: any writer stores 1
-    lds_bitonic(sk, CP);
-    for (int i = threadIdx.x; i < C; i += blockDim.x) ckeys[i] = sk[i];
-    if (threadIdx.x == 0) flag[0] = bad ? 0 : 1;
+    const int gt = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+    for (int i = gt; i < CP; i += nth) ckeys[i] = i < C ? sort_key(cpen[i], k + i) : ~0ull;
+    bool ok = true;
+    for (int i = gt; i + 1 < k; i += nth) ok &= (uint32_t)pen[i] <= (uint32_t)pen[i + 1];
+    ok = __syncthreads_and(ok);
+    if (threadIdx.x == 0) flag[blockIdx.x] = ok ? 1 : 0;
+}
+// every workgroup's flag set (call with blockDim >= kPrepBlocks, every thread)
+__device__ __forceinline__ bool survivors_sorted(const int32_t* flag) {
+    return __syncthreads_and(threadIdx.x < kPrepBlocks ? flag[threadIdx.x] != 0 : true);
 }
 
 // merge path: output i takes the i-th smallest of survivors (pen[a], a) and ckeys
 __global__ void replace_merge_kernel(const int32_t* __restrict__ pen, int N, int C, const uint64_t* __restrict__ ckeys,
                                      const int32_t* __restrict__ flag, uint64_t* __restrict__ mkeys) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= N || flag[0] == 0) return;
+    if (!survivors_sorted(flag) || i >= N) return;
     const int k = N - C;
     int lo = max(0, i - C), hi = min(i, k);
     while (lo < hi) {
@@ -231,10 +221,16 @@ __global__ void replace_merge_kernel(const int32_t* __restrict__ pen, int N, int
 
 // the fallback: full bitonic sort of keys[0..NP) by one workgroup in global memory
 // (keys, 8 B each, stay L2-resident); nothing to do when the merge ran
-__global__ __launch_bounds__(1024) void replace_fallback_sort_kernel(uint64_t* __restrict__ keys, int NP,
+__global__ __launch_bounds__(1024) void replace_fallback_sort_kernel(const int32_t* __restrict__ pen,
+                                                                     const int32_t* __restrict__ cpen, int C,
+                                                                     uint64_t* __restrict__ keys, int NP,
                                                                      const int32_t* __restrict__ flag,
                                                                      uint64_t* __restrict__ mkeys, int N) {
-    if (flag[0] != 0) return;
+    if (survivors_sorted(flag)) return;
+    for (int i = threadIdx.x; i < NP; i += blockDim.x)          // the keys (replace_keys_kernel's)
+        keys[i] = i >= N ? ~0ull : sort_key(i < N - C ? pen[i] : cpen[i - (N - C)], i);
+    __threadfence_block();
+    __syncthreads();
     for (int k = 2; k <= NP; k <<= 1)
         for (int j = k >> 1; j > 0; j >>= 1) {
             for (int q = threadIdx.x; q < NP / 2; q += blockDim.x) {
@@ -246,6 +242,127 @@ __global__ __launch_bounds__(1024) void replace_fallback_sort_kernel(uint64_t* _
             __syncthreads();
         }
     for (int i = threadIdx.x; i < N; i += blockDim.x) mkeys[i] = keys[i];
+}
+
+// ascending sort of tiles of T u64 keys (T a power of two, 2*KPT <= T <= kSortTile),
+// one workgroup of T/KPT threads per tile (tile blockIdx.x), the keys in registers
+// (TT_SORT_REG): thread t holds keys KPT*t..KPT*t+KPT-1; bitonic steps with j < KPT
+// run inside a thread, KPT <= j < 64*KPT between lanes of a wave (shuffles), larger
+// j between waves through LDS (double-buffered: one barrier per step).
+#ifndef TT_SORT_REG
+#define TT_SORT_REG 1
+#endif
+template <int KPT>
+__global__ __launch_bounds__(1024) void sort_reg_kernel(uint64_t* __restrict__ keys, int T) {
+    __shared__ uint64_t buf[KPT == 8 ? 2 : 1][KPT == 8 ? kSortTile : 1];
+    keys += (size_t)blockIdx.x * T;
+    const int t = threadIdx.x, nt = T / KPT;
+    const bool own = t < nt;
+    uint64_t v[KPT];
+#pragma unroll
+    for (int a = 0; a < KPT; ++a) v[a] = own ? keys[KPT * t + a] : ~0ull;
+    int par = 0;
+    for (int k = 2; k <= T; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {                 // uniform
+            if (j >= KPT) {
+                const int tj = j / KPT;                        // partner thread t ^ tj
+                uint64_t w[KPT];
+                if (KPT == 8 && tj >= 64) {                    // another wave: through LDS
+                    if (own) {
+#pragma unroll
+                        for (int a = 0; a < KPT; ++a) buf[par][KPT * t + a] = v[a];
+                    }
+                    __syncthreads();
+                    const int pt = own ? (t ^ tj) : t;
+#pragma unroll
+                    for (int a = 0; a < KPT; ++a) w[a] = buf[par][KPT * pt + a];
+                    par ^= 1;
+                } else {
+#pragma unroll
+                    for (int a = 0; a < KPT; ++a) w[a] = __shfl_xor(v[a], tj, 64);
+                }
+                const bool take_min = ((t & tj) == 0) == (((KPT * t) & k) == 0);
+#pragma unroll
+                for (int a = 0; a < KPT; ++a) v[a] = take_min ? (v[a] < w[a] ? v[a] : w[a]) : (v[a] < w[a] ? w[a] : v[a]);
+            } else {
+                // in-thread compare-exchanges with constant register indices (a runtime
+                // index would put v[] in indexed-register mode); branch-free selects
+                auto cx = [&](uint64_t& x, uint64_t& y, int a) {
+                    const bool u = ((KPT * t + a) & k) == 0;
+                    const uint64_t lo = x < y ? x : y, hi = x < y ? y : x;
+                    x = u ? lo : hi;
+                    y = u ? hi : lo;
+                };
+                if constexpr (KPT == 8) {
+                    if (j == 4) {
+                        cx(v[0], v[4], 0); cx(v[1], v[5], 1); cx(v[2], v[6], 2); cx(v[3], v[7], 3);
+                    } else if (j == 2) {
+                        cx(v[0], v[2], 0); cx(v[1], v[3], 1); cx(v[4], v[6], 4); cx(v[5], v[7], 5);
+                    } else {
+                        cx(v[0], v[1], 0); cx(v[2], v[3], 2); cx(v[4], v[5], 4); cx(v[6], v[7], 6);
+                    }
+                } else {
+                    if (j == 2) {
+                        cx(v[0], v[2], 0); cx(v[1], v[3], 1);
+                    } else {
+                        cx(v[0], v[1], 0); cx(v[2], v[3], 2);
+                    }
+                }
+            }
+        }
+    }
+    if (own) {
+#pragma unroll
+        for (int a = 0; a < KPT; ++a) keys[KPT * t + a] = v[a];
+    }
+}
+
+// ---- tiled form of the sort (TT_SORT_RANK) for kRankTile*2 <= NP <= kSortTile:
+// NP/kRankTile tiles sorted by one wave each (sort_reg_kernel<4>), then every key's
+// rank in the whole array counted directly from the sorted tiles -- key x at
+// position p of tile a has rank p + sum over tiles b < a of #{y <= x} + sum over
+// tiles b > a of #{y < x} (stable, so padding duplicates get distinct ranks) --
+// one lane per (key, tile), a binary search each, summed over the key's lanes.
+// Two launches spread over NP/kRankTile and NP*NT/256 workgroups instead of one
+// workgroup doing all 91 bitonic steps (64 us at 8,192 keys on one CU).
+#ifndef TT_SORT_RANK
+#define TT_SORT_RANK 1
+#endif
+constexpr int kRankTile = 256;
+
+// rank of keys[i] among keys[0..NP) (tiles of kRankTile sorted); every thread of
+// the group of NT lanes (NT = NP / kRankTile, a power of two <= 64) of key i calls it
+__device__ __forceinline__ int tile_rank(const uint64_t* __restrict__ keys, int i, int NT, int b, uint64_t& x) {
+    x = keys[i];
+    const int a = i / kRankTile;
+    int c;
+    if (b == a) {
+        c = i - a * kRankTile;
+    } else {
+        const uint64_t* tl = keys + (size_t)b * kRankTile;
+        const bool le = b < a;                                 // earlier tiles: count y <= x
+        c = 0;
+#pragma unroll
+        for (int s = kRankTile / 2; s >= 1; s >>= 1) {
+            const uint64_t y = tl[c + s - 1];
+            if (le ? y <= x : y < x) c += s;
+        }
+        const uint64_t y = tl[c];
+        if (c < kRankTile && (le ? y <= x : y < x)) ++c;
+    }
+    for (int o = 1; o < NT; o <<= 1) c += __shfl_xor(c, o, 64);
+    return c;
+}
+
+// sorted copy: out[rank(i)] = keys[i]
+__global__ __launch_bounds__(256) void rank_scatter_kernel(const uint64_t* __restrict__ keys, int NP, int NT,
+                                                           uint64_t* __restrict__ out) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = g / NT, b = g & (NT - 1);
+    if (i >= NP) return;                                       // whole groups (NP*NT is a multiple of 256)
+    uint64_t x;
+    const int r = tile_rank(keys, i, NT, b, x);
+    if (b == 0) out[r] = x;
 }
 
 // gather the sorted population into the work rows (one wave per row)
@@ -313,6 +430,17 @@ __global__ void lpt_order_kernel(const uint64_t* __restrict__ keys, int n, int32
     if (i < n) order[i] = (int32_t)(uint32_t)keys[i];
 }
 
+// order from tile-sorted keys: order[rank(i)] = index of key i (padding ranks >= n)
+__global__ __launch_bounds__(256) void lpt_rank_order_kernel(const uint64_t* __restrict__ keys, int NP, int NT, int n,
+                                                             int32_t* __restrict__ order) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = g / NT, b = g & (NT - 1);
+    if (i >= NP) return;
+    uint64_t x;
+    const int r = tile_rank(keys, i, NT, b, x);
+    if (b == 0 && r < n) order[r] = (int32_t)(uint32_t)x;
+}
+
 static int pow2_at_least(int n) {
     int p = 1;
     while (p < n) p <<= 1;
@@ -327,6 +455,10 @@ using namespace ttga;
 
 // ascending bitonic sort of NP (a power of two) u64 keys on stream st
 static void sort_keys(uint64_t* keys, int NP, hipStream_t st) {
+    if (TT_SORT_REG && NP >= 8 && NP <= kSortTile) {
+        hipLaunchKernelGGL(sort_reg_kernel<8>, dim3(1), dim3(std::max(64, NP / 8)), 0, st, keys, NP);
+        return;
+    }
     if (NP <= 4096) {
         hipLaunchKernelGGL(bitonic_lds_kernel, dim3(1), dim3(std::min(NP, 1024)), 0, st, keys, NP);
         return;
@@ -371,9 +503,17 @@ extern "C" int tt_ga_breed(const tt_problem* p, const uint8_t* pop_slot, const u
     return launch_mutation_masked(p, child_slot, child_room, rng, C, child_flags, kFlagMutate, st);
 }
 
+// NP keys in [2*kRankTile, kSortTile]: sorted by tiles + ranks (TT_SORT_RANK)
+static bool use_rank_sort(int NP) { return TT_SORT_RANK && NP >= 2 * kRankTile && NP <= kSortTile; }
+// the tiles of the rank sort (ranks are then counted by the caller's kernel)
+static void sort_rank_tiles(uint64_t* keys, int NP, hipStream_t st) {
+    hipLaunchKernelGGL(sort_reg_kernel<4>, dim3(NP / kRankTile), dim3(kRankTile / 4), 0, st, keys, kRankTile);
+}
+
 // work layout: sort keys [pow2(N)] u64 | slot rows [N][E] | room rows [N][E] |
 // meta [N][4] i32 | the source slot (256 B, written only by tt_ga_replace) |
-// merged keys [N] u64 | sorted child keys [kSortTile] u64 | merge flag (256 B)
+// merged keys [N] u64 | child keys [kSortTile] u64 | merge flag (256 B) |
+// sorted child keys [kSortTile] u64
 static size_t work_source_offset(int N, int E) {
     const size_t NP = (size_t)pow2_at_least(N);
     return align256(8 * NP) + 2 * align256((size_t)N * E) + align256(16 * (size_t)N);
@@ -382,7 +522,7 @@ static size_t work_merge_offset(int N, int E) { return work_source_offset(N, E) 
 
 extern "C" size_t tt_ga_work_bytes(int N, int E) {
     if (N < 1 || E < 1) return 0;
-    return work_merge_offset(N, E) + align256(8 * (size_t)N) + 8 * (size_t)kSortTile + 256;
+    return work_merge_offset(N, E) + align256(8 * (size_t)N) + 16 * (size_t)kSortTile + 256;
 }
 
 extern "C" size_t tt_ga_work_source_offset(int N, int E) {
@@ -410,21 +550,32 @@ extern "C" int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* po
     uint8_t* ws = w + align256(8 * (size_t)NP);
     uint8_t* wr = ws + align256((size_t)N * E);
     int32_t* wm = (int32_t*)(wr + align256((size_t)N * E));
-    hipLaunchKernelGGL(replace_keys_kernel, dim3((NP + 255) / 256), dim3(256), 0, st, pop_penalty, child_penalty, N, C,
-                       NP, keys);
     const uint64_t* sorted = keys;
     if (TT_GA_MERGE && C <= kSortTile) {
         uint64_t* mkeys = (uint64_t*)(w + work_merge_offset(N, E));
         uint64_t* ckeys = (uint64_t*)((uint8_t*)mkeys + align256(8 * (size_t)N));
         int32_t* flag = (int32_t*)(ckeys + kSortTile);
         const int CP = pow2_at_least(std::max(C, 2));
-        hipLaunchKernelGGL(replace_prep_kernel, dim3(1), dim3(1024), 0, st, pop_penalty, child_penalty, N, C, CP, ckeys,
-                           flag);
-        hipLaunchKernelGGL(replace_merge_kernel, dim3((N + 255) / 256), dim3(256), 0, st, pop_penalty, N, C, ckeys, flag,
-                           mkeys);
-        hipLaunchKernelGGL(replace_fallback_sort_kernel, dim3(1), dim3(1024), 0, st, keys, NP, flag, mkeys, N);
+        hipLaunchKernelGGL(replace_prep_kernel, dim3(kPrepBlocks), dim3(256), 0, st, pop_penalty, child_penalty, N, C, CP,
+                           ckeys, flag);
+        const uint64_t* csorted = ckeys;
+        if (use_rank_sort(CP)) {
+            uint64_t* cs2 = (uint64_t*)((uint8_t*)flag + 256);
+            const int NT = CP / kRankTile;
+            sort_rank_tiles(ckeys, CP, st);
+            hipLaunchKernelGGL(rank_scatter_kernel, dim3(CP * NT / 256), dim3(256), 0, st, ckeys, CP, NT, cs2);
+            csorted = cs2;
+        } else {
+            sort_keys(ckeys, CP, st);
+        }
+        hipLaunchKernelGGL(replace_merge_kernel, dim3((N + 255) / 256), dim3(256), 0, st, pop_penalty, N, C, csorted,
+                           flag, mkeys);
+        hipLaunchKernelGGL(replace_fallback_sort_kernel, dim3(1), dim3(1024), 0, st, pop_penalty, child_penalty, C, keys,
+                           NP, flag, mkeys, N);
         sorted = mkeys;
     } else {
+        hipLaunchKernelGGL(replace_keys_kernel, dim3((NP + 255) / 256), dim3(256), 0, st, pop_penalty, child_penalty, N,
+                           C, NP, keys);
         sort_keys(keys, NP, st);
     }
     hipLaunchKernelGGL(replace_gather_kernel, dim3(N), dim3(64), 0, st, E, N, C, sorted, pop_slot, pop_room, pop_hcv,
@@ -447,6 +598,12 @@ extern "C" int tt_lpt_order(const tt_problem* p, const int32_t* key, int n, int3
     const int NP = pow2_at_least(n);
     uint64_t* keys = (uint64_t*)work;
     hipLaunchKernelGGL(lpt_keys_kernel, dim3((NP + 255) / 256), dim3(256), 0, st, key, n, NP, keys);
+    if (use_rank_sort(NP)) {
+        const int NT = NP / kRankTile;
+        sort_rank_tiles(keys, NP, st);
+        hipLaunchKernelGGL(lpt_rank_order_kernel, dim3(NP * NT / 256), dim3(256), 0, st, keys, NP, NT, n, order);
+        return check_hip(hipGetLastError(), "tt_lpt_order launch");
+    }
     sort_keys(keys, NP, st);
     hipLaunchKernelGGL(lpt_order_kernel, dim3((n + 255) / 256), dim3(256), 0, st, keys, n, order);
     return check_hip(hipGetLastError(), "tt_lpt_order launch");

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -30,6 +31,9 @@ struct tt_problem {
     };
     std::vector<LsRedo> ls_redo;
     std::mutex ls_mu;
+    // students with phase-2 masks in the local search, per matcher-task cap
+    // (full, small); -1 until the first call decides (tt_ls.hip ls_mask_students)
+    std::atomic<int> ls_smask[2] = {-1, -1};
 };
 
 namespace ttga {

@@ -57,14 +57,37 @@ __device__ unsigned long long g_ls_prof[kPfN];
 #endif
 
 struct LsLayout {
-    size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, cnt, task, slp, pos;
+    size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, cnt, task, slp, pos, ps, sm;
     size_t task_bytes;
     int NT;              // events per matcher task (min(E, 256))
     size_t bytes;
 };
 
+// TT_LS_POSS16: every event's possibleRooms mask copied into LDS as u16 when
+// R <= 16 (0.8 KB per wave at E = 400), so a matcher task's masks and the
+// phase-2 augmenting-path test read LDS instead of waiting on L2. Same-box A/B
+// (profiles/r03_s11_ab.json): comp01 phase 1 -3 %, med phase 2 +5 % (one fewer
+// wave per CU); off
+#ifndef TT_LS_POSS16
+#define TT_LS_POSS16 0
+#endif
+// TT_LS_SMASK: in phase 2 the state is feasible, so no student has two events
+// in one slot and a student's 45-bit attendance mask changes by clearing the old
+// and setting the new slot of a moved event. The masks of all students are kept
+// in LDS for phase 2 (S <= 512), and eventScv / singleClassesScv read a student's
+// mask instead of rebuilding it from the student's event list. The host turns
+// them on (smS = S) only where the S*8 bytes of LDS cost no resident waves
+// (ls_mask_students): same-box A/B at pop 4,096 / 8,192 (profiles/r03_s13_ab.json)
+// med phase-2 LS(1000) -9 % (16 waves per CU fit either way), comp01 and lg +12..18 %
+// (a second round of waves); at pop 65,536 (profiles/r03_s14_ab.json) forced masks
+// gave med -2 %, comp01 +18 %, lg +33 %.
+#ifndef TT_LS_SMASK
+#define TT_LS_SMASK 1
+#endif
+constexpr size_t kSmaskMaxBytes = 4096;
 // cap: events per matcher task (kLsCapSmall for the first launch, kMaxSlotEvents for the redo launch)
-__host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap) {
+// S: students with phase-2 masks (0: none)
+__host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap, int S) {
     LsLayout L;
     size_t b = 0;
     auto al = [&](size_t a) { b = (b + a - 1) & ~(a - 1); };
@@ -78,7 +101,18 @@ __host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap) {
 #else
     L.pos = L.slp = 0;
 #endif
-    al(8); L.B = b; b += 8 * (size_t)kSlots * EW;
+#if TT_LS_POSS16
+    L.ps = b; if (R <= 16) b += 2 * (size_t)E;        // possibleRooms as u16 (R <= 16)
+#else
+    L.ps = 0;
+#endif
+    al(8);
+#if TT_LS_SMASK
+    L.sm = b; if (S > 0 && 8 * (size_t)S <= kSmaskMaxBytes) b += 8 * (size_t)S;   // phase-2 student masks (S = smS)
+#else
+    L.sm = 0;
+#endif
+    L.B = b; b += 8 * (size_t)kSlots * EW;
     L.NB = b; b += 8 * (size_t)kLsTasks * EW;
     L.rp = b; b += 4 * (size_t)kSlots;
     L.hist = b; b += 2 * (size_t)kSlots * R;
@@ -112,6 +146,8 @@ struct LsState {
     uint16_t* pos;       // [E] position of each event in evl (TT_LS_SLP)
     uint8_t* slp;        // [E] slot of the event at each position (TT_LS_SLP)
     uint64_t *B, *NB;
+    const uint16_t* ps;  // [E] possibleRooms in LDS (R <= 16), else null (TT_LS_POSS16)
+    uint64_t* sm;        // [S] phase-2 attendance masks (TT_LS_SMASK), null outside phase 2
     int32_t* rp;
     uint16_t* hist;
     int32_t* misc;       // [0..2] neighbour room pairs per task, [3] redo flag, [4..6] events per task
@@ -144,6 +180,10 @@ __device__ __forceinline__ LsTask get_task(const LsState& S, int k) {
     T.rm = (uint8_t*)(T.hist + S.R);
     T.dr = T.rm + S.R;
     return T;
+}
+
+__device__ __forceinline__ uint64_t poss_of(const LsState& S, int e) {
+    return S.ps ? (uint64_t)S.ps[e] : S.pb.poss[e];
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -204,6 +244,17 @@ __device__ __forceinline__ int ehcv_cur(LsState& S, int e) {
 
 // eventScv(e) and singleClassesScv(e) (Solution.cpp:248-355) in the current
 // (nb = false) or neighbour (nb = true) state.
+// student st attends event q (its padded event list holds q)
+__device__ __forceinline__ bool attends(const DevProblem& pb, int st, int q) {
+    bool f = false;
+    const int c0 = pb.stc_off[st], c1 = pb.stc_off[st + 1];
+    for (int c = c0; c < c1; c += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f |= pb.stc_ev[c + j] == q;
+    }
+    return f;
+}
+
 __device__ __forceinline__ void scv_terms(LsState& S, int e, bool nb, int& es, int& scs) {
     LSP_T(t0);
     const DevProblem& pb = S.pb;
@@ -211,16 +262,42 @@ __device__ __forceinline__ void scv_terms(LsState& S, int e, bool nb, int& es, i
     const int day = t / 9, pos = t - 9 * day;
     const int k0 = pb.ev_off[e], k1 = pb.ev_off[e + 1];
     int a = 0, b = 0;
+    // phase-2 masks: the neighbour's mask of a student of e clears the old and sets the
+    // new slot of every moved event the student attends -- e itself, and any other moved
+    // event correlated with e (a shared student); clears before sets (a swap keeps both)
+    int oth = 0;                                       // bit q: moved event q != e correlated with e
+    if (S.sm && nb) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            if (q >= S.nmv) break;
+            const int qe = S.mv_e[q];
+            if (qe != e && ((pb.corr64[(size_t)e * S.EW + (qe >> 6)] >> (qe & 63)) & 1ull)) oth |= 1 << q;
+        }
+    }
     for (int k = k0 + S.lane; k < k1; k += 64) {
         const int st = pb.ev_stu[k];
         uint64_t m = 0;
-        const int c0 = pb.stc_off[st], c1 = pb.stc_off[st + 1];
-        for (int c = c0; c < c1; c += 8) {
-            int ev[8];
+        if (S.sm) {
+            m = S.sm[st];
+            if (nb) {
+                uint64_t clr = 1ull << S.sl[e], set = 1ull << t;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) ev[j] = pb.stc_ev[c + j];
+                for (int q = 0; q < 3; ++q) {
+                    if (!((oth >> q) & 1)) continue;
+                    const int qe = S.mv_e[q];
+                    if (attends(pb, st, qe)) { clr |= 1ull << S.sl[qe]; set |= 1ull << S.mv_t[q]; }
+                }
+                m = (m & ~clr) | set;
+            }
+        } else {
+            const int c0 = pb.stc_off[st], c1 = pb.stc_off[st + 1];
+            for (int c = c0; c < c1; c += 8) {
+                int ev[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) m |= 1ull << ((nb ? slot_nb(S, ev[j]) : S.sl[ev[j]]) & 63);
+                for (int j = 0; j < 8; ++j) ev[j] = pb.stc_ev[c + j];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) m |= 1ull << ((nb ? slot_nb(S, ev[j]) : S.sl[ev[j]]) & 63);
+            }
         }
         const uint32_t dm = (uint32_t)(m >> (9 * day)) & 0x1FFu;
         const uint32_t others = dm & ~(1u << pos);
@@ -502,7 +579,7 @@ __device__ __forceinline__ TaskRegs load_tasks(LsState& S, int kmask) {
         r.tn[k] = k < S.nts && ((kmask >> k) & 1) ? S.misc[4 + k] : 0;
         const bool a = S.lane < r.tn[k] && r.tn[k] <= 64;
         r.tev[k] = a ? get_task(S, k).ev[S.lane] : 0;
-        r.tpl[k] = a ? S.pb.poss[r.tev[k]] : 0ull;
+        r.tpl[k] = a ? poss_of(S, r.tev[k]) : 0ull;
     }
     return r;
 }
@@ -620,6 +697,22 @@ __device__ __forceinline__ void cache_drop(LsState& S) {
 __device__ __forceinline__ void accept(LsState& S) {
     LSP_T(t0);
     S.c1_valid = 0;
+    if (S.sm) {                       // phase-2 masks: clear every moved event's old slot, then set the new ones
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            if (q >= S.nmv) break;
+            const int qe = S.mv_e[q];
+            const uint64_t c = ~(1ull << S.sl[qe]);
+            for (int k = S.pb.ev_off[qe] + S.lane; k < S.pb.ev_off[qe + 1]; k += 64) S.sm[S.pb.ev_stu[k]] &= c;
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            if (q >= S.nmv) break;
+            const int qe = S.mv_e[q];
+            const uint64_t st_bit = 1ull << S.mv_t[q];
+            for (int k = S.pb.ev_off[qe] + S.lane; k < S.pb.ev_off[qe + 1]; k += 64) S.sm[S.pb.ev_stu[k]] |= st_bit;
+        }
+    }
     sync_rooms(S, true);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -791,10 +884,10 @@ __device__ __forceinline__ bool matchable(LsState& S, int s, int out, int a) {
     const int R = S.R, lane = S.lane;
     const int o = lane < R ? (int)S.hist[s * R + lane] : 0xFFFF;
     const bool valid = o != 0xFFFF && o != out;
-    const uint64_t po = valid ? S.pb.poss[o] : 0ull;
+    const uint64_t po = valid ? poss_of(S, o) : 0ull;
     const uint64_t used = ballot(valid);
     const uint64_t fre = (R >= 64 ? ~0ull : ((1ull << R) - 1)) & ~used;
-    uint64_t seen = S.pb.poss[a];
+    uint64_t seen = poss_of(S, a);
     if (seen & fre) return true;
     uint64_t fr = seen & used;
     while (fr) {
@@ -857,7 +950,7 @@ template <int CAP>
 __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& pb, uint8_t* __restrict__ slot,
                                                              uint8_t* __restrict__ room, int64_t* __restrict__ rng,
                                                              long p, int max_steps, double p1, double p2, double p3,
-                                                             int32_t* __restrict__ redo_list) {
+                                                             int32_t* __restrict__ redo_list, int smS) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int E = pb.E, R = pb.R, EW = pb.EW64;
     const int lane = threadIdx.x;
@@ -865,13 +958,15 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
 #ifdef TT_LS_PROF
     uint64_t t_ph = 0;                  // phase timer (assigned, not declared, between the gotos and redo:)
 #endif
-    const LsLayout L = ls_layout(E, R, EW, CAP);
+    const LsLayout L = ls_layout(E, R, EW, CAP, smS);
     LsState S;
     S.pb = pb; S.E = E; S.R = R; S.EW = EW; S.lane = lane;
     S.sl = lds + L.sl; S.rr = lds + L.rr; S.nrr = lds + L.nrr;
     S.evl = (uint16_t*)(lds + L.evl);
     S.pos = (uint16_t*)(lds + L.pos); S.slp = lds + L.slp;
     S.B = (uint64_t*)(lds + L.B); S.NB = (uint64_t*)(lds + L.NB);
+    S.ps = (TT_LS_POSS16 && R <= 16) ? (const uint16_t*)(lds + L.ps) : nullptr;
+    S.sm = nullptr;
     S.rp = (int32_t*)(lds + L.rp); S.hist = (uint16_t*)(lds + L.hist);
     S.misc = (int32_t*)(lds + L.misc);
     S.cnt = (uint32_t*)(lds + L.cnt);
@@ -897,6 +992,8 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
         S.sl[e] = s; S.rr[e] = r; S.nrr[e] = r; S.evl[e] = (uint16_t)e;
     }
     if (lane == 0) S.sl[E] = 63;
+    if (S.ps)
+        for (int e = lane; e < E; e += 64) ((uint16_t*)S.ps)[e] = (uint16_t)pb.poss[e];
     for (int c = lane; c < kSlots * EW; c += 64) S.B[c] = 0ull;
     for (int c = lane; c < kSlots * R; c += 64) S.hist[c] = 0;
     __syncthreads();
@@ -1177,6 +1274,14 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
         // owner table in place of the room histogram (rooms are distinct per slot now)
         S.phase2 = 1;
         for (int c = lane; c < kSlots * R; c += 64) S.hist[c] = 0xFFFF;
+        if (TT_LS_SMASK && smS > 0) {
+            S.sm = (uint64_t*)(lds + L.sm);
+            for (int st = lane; st < pb.S; st += 64) {
+                uint64_t m = 0;
+                for (int c = pb.stc_off[st]; c < pb.stc_off[st + 1]; ++c) m |= 1ull << (S.sl[pb.stc_ev[c]] & 63);
+                S.sm[st] = m;
+            }
+        }
         wave_sync();
         for (int e = lane; e < E; e += 64) S.hist[S.sl[e] * R + S.rr[e]] = (uint16_t)e;
         wave_sync();
@@ -1392,23 +1497,26 @@ redo:
 template <int CAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE))) void local_search_kernel(
     DevProblem pb, uint8_t* __restrict__ slot, uint8_t* __restrict__ room, int64_t* __restrict__ rng, int P,
-    int max_steps, double p1, double p2, double p3, int32_t* __restrict__ redo_list, const int32_t* __restrict__ order) {
+    int max_steps, double p1, double p2, double p3, int32_t* __restrict__ redo_list, const int32_t* __restrict__ order,
+    int smS) {
     const long p = order ? (long)order[blockIdx.x] : (long)blockIdx.x;   // dispatch order only
     if ((unsigned long)p >= (unsigned long)P) return;
-    ls_one<CAP>(pb, slot, room, rng, p, max_steps, p1, p2, p3, redo_list);
+    ls_one<CAP>(pb, slot, room, rng, p, max_steps, p1, p2, p3, redo_list, smS);
 }
 
 // Redo launch: a grid of resident waves works through the individuals the
 // first launch listed, with full-size matcher tasks; the last wave to finish
-// resets the list for the stream's next call (no per-call memset). An empty
-// list costs one short launch.
+// resets the list for the stream's next call (no per-call memset). With an
+// empty list every wave returns at once (the arrival count is only needed when
+// there is a list to reset: 52 -> a few us per GA generation).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE))) void local_search_redo_kernel(
     DevProblem pb, uint8_t* __restrict__ slot, uint8_t* __restrict__ room, int64_t* __restrict__ rng, int max_steps,
-    double p1, double p2, double p3, int32_t* __restrict__ redo_list) {
+    double p1, double p2, double p3, int32_t* __restrict__ redo_list, int smS) {
     const int n = redo_list[0];
+    if (n == 0) return;             // nothing listed: every wave sees 0, no reset needed (no arrival atomics)
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         __syncthreads();
-        ls_one<kMaxSlotEvents>(pb, slot, room, rng, (long)redo_list[2 + i], max_steps, p1, p2, p3, nullptr);
+        ls_one<kMaxSlotEvents>(pb, slot, room, rng, (long)redo_list[2 + i], max_steps, p1, p2, p3, nullptr, smS);
     }
     __threadfence();
     if (threadIdx.x == 0 && atomicAdd(&redo_list[1], 1) == (int)gridDim.x - 1) {
@@ -1466,6 +1574,37 @@ extern "C" int tt_ls_prof_read(unsigned long long* out, int reset) {
 }
 #endif
 
+// Phase-2 masks for kernel k at cap: the workgroups per CU without and with
+// them, (o0 << 8) | o1 (0: no masks for this instance)
+template <typename K>
+static int ls_mask_occupancy(const tt_problem* p, int cap, K k) {
+    const int S = p->dev.S;
+    if (!TT_LS_SMASK || S <= 0 || 8 * (size_t)S > kSmaskMaxBytes) return 0;
+    const size_t b0 = ls_layout(p->E, p->R, p->dev.EW64, cap, 0).bytes, b1 = ls_layout(p->E, p->R, p->dev.EW64, cap, S).bytes;
+    int o0 = 0, o1 = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o0, k, 64, b0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, k, 64, b1) != hipSuccess || o1 < 1)
+        return 0;
+    return (std::min(o0, 255) << 8) | std::min(o1, 255);
+}
+
+// students with phase-2 masks for a launch of P waves: S where the masks cost no
+// resident waves -- the same occupancy with them, or P small enough that every
+// CU holds all its waves at once with them -- else 0 (memoised per problem)
+template <typename K>
+static int ls_mask_students(const tt_problem* p, int cap, K k, int P) {
+    std::atomic<int>& memo = const_cast<tt_problem*>(p)->ls_smask[cap == kMaxSlotEvents ? 0 : 1];
+    int m = memo.load(std::memory_order_relaxed);
+    if (m < 0) memo.store(m = ls_mask_occupancy(p, cap, k), std::memory_order_relaxed);
+    if (m == 0) return 0;
+#ifdef TT_LS_SMASK_FORCE
+    return p->dev.S;                            // profiling: masks whatever the occupancy
+#endif
+    const int o0 = m >> 8, o1 = m & 255;
+    const long per_cu = ((long)P + p->num_cus - 1) / p->num_cus;
+    return (o1 >= o0 || per_cu <= o1) ? p->dev.S : 0;
+}
+
 extern "C" int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P,
                                int max_steps, double p1, double p2, double p3, void* stream) {
     return tt_local_search_ordered(p, slot, room, rng, P, max_steps, p1, p2, p3, nullptr, stream);
@@ -1479,7 +1618,8 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
     if (!rng) { set_error("null rng buffer"); return TT_ERR_INVALID; }
     if (max_steps < 0) { set_error("negative max_steps"); return TT_ERR_INVALID; }
     if ((rc = use_device(p))) return rc;
-    const LsLayout Lf = ls_layout(p->E, p->R, p->dev.EW64, kMaxSlotEvents);
+    const int smf = ls_mask_students(p, kMaxSlotEvents, local_search_kernel<kMaxSlotEvents>, P);
+    const LsLayout Lf = ls_layout(p->E, p->R, p->dev.EW64, kMaxSlotEvents, smf);
     if (Lf.bytes > 160 * 1024) { set_error("instance too large for the local-search kernel"); return TT_ERR_LIMIT; }
     hipStream_t st = (hipStream_t)stream;
     if (order) {
@@ -1488,10 +1628,11 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
     }
     if (p->E <= kLsCapSmall) {                      // no slot can exceed the small tasks
         hipLaunchKernelGGL(local_search_kernel<kMaxSlotEvents>, dim3(P), dim3(64), Lf.bytes, st, p->dev, slot, room,
-                           rng, P, max_steps, p1, p2, p3, (int32_t*)nullptr, order);
+                           rng, P, max_steps, p1, p2, p3, (int32_t*)nullptr, order, smf);
         return check_hip(hipGetLastError(), "local_search launch");
     }
-    const LsLayout Ls = ls_layout(p->E, p->R, p->dev.EW64, kLsCapSmall);
+    const int sms = ls_mask_students(p, kLsCapSmall, local_search_kernel<kLsCapSmall>, P);
+    const LsLayout Ls = ls_layout(p->E, p->R, p->dev.EW64, kLsCapSmall, sms);
     tt_problem* mp = const_cast<tt_problem*>(p);
     std::lock_guard<std::mutex> lock(mp->ls_mu);
     // this stream's redo list (grown stream-ordered: the old one may still be read)
@@ -1511,14 +1652,14 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
         rl->cap = P;
     }
     hipLaunchKernelGGL(local_search_kernel<kLsCapSmall>, dim3(P), dim3(64), Ls.bytes, st, p->dev, slot, room, rng, P,
-                       max_steps, p1, p2, p3, rl->list, order);
+                       max_steps, p1, p2, p3, rl->list, order, sms);
     TT_HIP(hipGetLastError());
     // the redo launch: resident waves only (an empty list costs one short launch)
     int per_cu = 0;
     TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, local_search_redo_kernel, 64, Lf.bytes));
     const int grid = std::min(P, std::max(1, per_cu) * p->num_cus);
     hipLaunchKernelGGL(local_search_redo_kernel, dim3(grid), dim3(64), Lf.bytes, st, p->dev, slot, room, rng,
-                       max_steps, p1, p2, p3, rl->list);
+                       max_steps, p1, p2, p3, rl->list, smf);
     TT_HIP(hipGetLastError());
     return TT_OK;
 }

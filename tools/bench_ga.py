@@ -65,7 +65,10 @@ ap.add_argument("--warm-gens", type=int, default=0, help="at most this many unti
 ap.add_argument("--warm-feasible", type=float, default=1.1, help="stop warming once this fraction is feasible")
 ap.add_argument("--lpt", choices=["auto", "on", "off"], default="auto",
                 help="longest-expected-first dispatch of the children's local search (Island default: auto)")
+ap.add_argument("--lib", default=None, help="profiling: an A/B build (tools/ab_build.sh) instead of the in-tree library")
 a = ap.parse_args()
+if a.lib:
+    native._lib = native.load(pathlib.Path(a.lib).resolve())
 
 inst = ttga.config_instance(a.config)
 dp = native.DeviceProblem(inst)

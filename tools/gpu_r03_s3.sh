@@ -6,7 +6,5 @@ set -u
 export TMPDIR=/tmp
 T=${1:-r03_s3}; O=gpurun_out/$T; mkdir -p $O
 step() { local n=$1 lim=$2; shift 2; echo "== $n"; timeout -k 10 $lim "$@" > $O/$n.log 2>&1; local rc=$?; echo "== $n rc=$rc"; tail -c 1500 $O/$n.log; echo; [ $rc -ge 124 ] && exit $rc; return 0; }
-step dbg1 120 python -u tools/dbg_lanes.py head lanesvm
-step dbg2 120 python -u tools/dbg_lanes.py head vm2
 step lsprof_ga 300 python -u tools/ls_prof.py --config comp01 --pop 65536 --children 8192 --from-ga 0.6 --steps 1000
 echo done
