@@ -142,7 +142,19 @@ __device__ inline void build_buckets(const DevProblem& pb, MatchScratch& m, int 
 #endif
     __syncthreads();
     const int nb = m.bstart[kSlots];
-    for (int b = lane; b < nb; b += 64) m.pl[b] = pb.poss[m.bev[b]];
+    for (int b0 = 0; b0 < nb; b0 += 512) {            // eight gathers in flight per block
+        uint64_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int b = b0 + 64 * k + lane;
+            v[k] = b < nb ? pb.poss[m.bev[b]] : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int b = b0 + 64 * k + lane;
+            if (b < nb) m.pl[b] = v[k];
+        }
+    }
     __syncthreads();
 }
 
@@ -242,6 +254,107 @@ __device__ void match_slot(int R, const uint16_t* ev, const uint64_t* pl, int N,
     }
 }
 
+// match_slot for N <= 32 events and R <= 16 rooms (TT_MATCH_REG) with the
+// matching itself in registers: the matched room of each event as 4-bit fields
+// (mr0: events 0-15, mr1: 16-31; valid while the event's bit is clear in unm)
+// and the event matched to each room as 8-bit fields (rm0: rooms 0-7, rm1:
+// 8-15). The lane-serial search then waits on LDS only for an event's
+// possible rooms (and writes its dads there, read back on the augmenting path):
+// a room expansion and the path's matched-room lookups are register selects.
+// Same search, same result as match_slot.
+#ifndef TT_MATCH_REG
+#define TT_MATCH_REG 1
+#endif
+__device__ __forceinline__ uint32_t nib_get(uint64_t w0, uint64_t w1, int i) {
+    return (uint32_t)(((i < 16 ? w0 : w1) >> (4 * (i & 15))) & 15ull);
+}
+__device__ __forceinline__ void nib_set(uint64_t& w0, uint64_t& w1, int i, uint32_t v) {
+    const int sh = 4 * (i & 15);
+    const uint64_t clr = ~(15ull << sh), put = (uint64_t)v << sh;
+    if (i < 16) w0 = (w0 & clr) | put;
+    else w1 = (w1 & clr) | put;
+}
+__device__ __forceinline__ uint32_t byte_get(uint64_t w0, uint64_t w1, int j) {
+    return (uint32_t)(((j < 8 ? w0 : w1) >> (8 * (j & 7))) & 255ull);
+}
+__device__ __forceinline__ void byte_set(uint64_t& w0, uint64_t& w1, int j, uint32_t v) {
+    const int sh = 8 * (j & 7);
+    const uint64_t clr = ~(255ull << sh), put = (uint64_t)v << sh;
+    if (j < 8) w0 = (w0 & clr) | put;
+    else w1 = (w1 & clr) | put;
+}
+
+__device__ void match_slot_reg(const uint16_t* ev, const uint64_t* pl, int N, uint8_t* dr, uint8_t* rr) {
+    uint32_t unm = N >= 32 ? ~0u : ((1u << N) - 1u);
+    uint64_t mr0 = 0, mr1 = 0, rm0 = 0, rm1 = 0;
+    uint32_t rmatched = 0;
+    for (;;) {
+        // networkFlow (Solution.cpp:852-891): lowest-index-first search from the source
+        uint32_t se = unm, fe = unm, sr = 0, fr = 0;
+        int sink = -1;
+        for (;;) {
+            if (fe) {                                  // expand event i: forward residual edges
+                const int i = __builtin_ctz(fe);
+                fe &= fe - 1;
+                const uint32_t own = ((unm >> i) & 1u) ? 0u : (1u << nib_get(mr0, mr1, i));
+                uint32_t nr = (uint32_t)pl[i] & ~sr & ~own;
+                sr |= nr;
+                fr |= nr;
+                while (nr) {
+                    const int j = __builtin_ctz(nr);
+                    nr &= nr - 1;
+                    dr[j] = (uint8_t)i;
+                }
+                continue;
+            }
+            if (fr) {                                  // expand room j
+                const int j = __builtin_ctz(fr);
+                fr &= fr - 1;
+                if (!((rmatched >> j) & 1u)) { sink = j; break; }   // free room: path to the sink is fixed
+                const uint32_t b = 1u << byte_get(rm0, rm1, j);     // reverse edge to its matched event
+                if (!(se & b)) { se |= b; fe |= b; }
+                continue;
+            }
+            break;
+        }
+        if (sink < 0) break;
+        // maxMatching augmentation (Solution.cpp:836-849)
+        int j = sink;
+        for (;;) {
+            const int i = dr[j];
+            const bool was = !((unm >> i) & 1u);
+            const int prev = (int)nib_get(mr0, mr1, i);
+            nib_set(mr0, mr1, i, (uint32_t)j);
+            byte_set(rm0, rm1, j, (uint32_t)i);
+            rmatched |= 1u << j;
+            if (!was) {
+                unm &= ~(1u << i);
+                break;
+            }
+            j = prev;
+        }
+    }
+    // read-out and unplaced events (Solution.cpp:802-830)
+    int less_busy = 0;
+    for (int i = 0; i < N; ++i) {
+        int r;
+        if (!((unm >> i) & 1u)) {
+            r = (int)nib_get(mr0, mr1, i);
+        } else {
+            const uint64_t ps = pl[i];
+            if (ps) {
+                less_busy = __builtin_ctzll(ps);
+                if ((rmatched >> less_busy) & 1u) {
+                    const uint64_t fr2 = ps & ~(uint64_t)rmatched;
+                    if (fr2) less_busy = __builtin_ctzll(fr2);
+                }
+            }
+            r = less_busy;
+        }
+        rr[ev[i]] = (uint8_t)r;
+    }
+}
+
 // Re-assign rooms for every slot t with bit t of `touched` set and a
 // non-empty bucket. m.sl and m.rr hold the individual's row; rooms of
 // untouched slots in m.rr are left as they are. Buckets must be built.
@@ -251,7 +364,9 @@ __device__ inline void assign_touched(const DevProblem& pb, MatchScratch& m, uin
         const int N = m.bstart[lane + 1] - b0;
         const int R = pb.R;
         if (N > 0) {
-            if (N <= 64)
+            if (TT_MATCH_REG && N <= 32 && R <= 16)
+                match_slot_reg(m.bev + b0, m.pl + b0, N, m.dr + lane * R, m.rr);
+            else if (N <= 64)
                 match_slot<1>(R, m.bev + b0, m.pl + b0, N, m.mr + b0, m.rm + lane * R, m.dr + lane * R, m.rr);
             else if (N <= kMaxSlotEvents)
                 match_slot<4>(R, m.bev + b0, m.pl + b0, N, m.mr + b0, m.rm + lane * R, m.dr + lane * R, m.rr);

@@ -14,8 +14,22 @@ constexpr int kMaxRejections = 1 << 20;
 #endif
 
 // ---------------------------------------------------------------- helpers
+// 512 bytes per block: the block's eight loads are all in flight before the
+// first LDS store (a plain loop waits out one HBM latency per 64 bytes)
 __device__ inline void load_row(uint8_t* dst, const uint8_t* src, int E, int lane) {
-    for (int e = lane; e < E; e += 64) dst[e] = src[e];
+    for (int e0 = 0; e0 < E; e0 += 512) {
+        uint8_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int e = e0 + 64 * k + lane;
+            v[k] = e < E ? src[e] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int e = e0 + 64 * k + lane;
+            if (e < E) dst[e] = v[k];
+        }
+    }
 }
 
 __device__ inline void store_row(uint8_t* dst, const uint8_t* src, int E, int lane) {
