@@ -168,11 +168,17 @@ def test_assign_rooms_golden(problems, name):
 
 
 def test_assign_rooms_random_vs_oracle(orc):
-    for seed, dims in [(21, (250, 12, 4, 150)), (22, (600, 30, 6, 300))]:
+    # R = 16 / 17 and slots of exactly 32 / 33 events sit on the register
+    # matcher's limits (N <= 32, R <= 16, TT_MATCH_REG), crowded slots past them
+    for seed, dims in [(21, (250, 12, 4, 150)), (22, (600, 30, 6, 300)), (23, (300, 16, 4, 150)),
+                       (24, (300, 17, 4, 150))]:
         inst = ttga.generate(*dims, seed=seed)
         dp = native.DeviceProblem(inst)
         slots, _ = ttga.random_slots(ttga.population_seeds(seed, 97), inst.E)
         slots[:10] = (slots[:10] % 4) * 11     # crowded slots
+        for r, n in ((10, 32), (11, 33), (12, 31)):
+            slots[r, :n] = 7
+            slots[r, n:] = np.where(slots[r, n:] == 7, 8, slots[r, n:])
         assert np.array_equal(host(dp.assign_rooms(dev(slots))), orc.problem(inst).assign_rooms(slots))
 
 

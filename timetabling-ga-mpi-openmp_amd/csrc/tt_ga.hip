@@ -365,6 +365,27 @@ __global__ __launch_bounds__(256) void rank_scatter_kernel(const uint64_t* __res
     if (b == 0) out[r] = x;
 }
 
+// copy two rows of E bytes (slot and room), 512 bytes per lane block with all
+// loads in flight before the stores
+__device__ __forceinline__ void copy_rows2(uint8_t* __restrict__ d0, const uint8_t* __restrict__ s0,
+                                           uint8_t* __restrict__ d1, const uint8_t* __restrict__ s1, int E,
+                                           int lane) {
+    for (int e0 = 0; e0 < E; e0 += 512) {
+        uint8_t a[8], b[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int e = e0 + 64 * k + lane;
+            a[k] = e < E ? s0[e] : 0;
+            b[k] = e < E ? s1[e] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int e = e0 + 64 * k + lane;
+            if (e < E) { d0[e] = a[k]; d1[e] = b[k]; }
+        }
+    }
+}
+
 // gather the sorted population into the work rows (one wave per row)
 __global__ __launch_bounds__(64) void replace_gather_kernel(int E, int N, int C, const uint64_t* __restrict__ keys,
                                                             const uint8_t* __restrict__ ps, const uint8_t* __restrict__ pr,
@@ -383,10 +404,7 @@ __global__ __launch_bounds__(64) void replace_gather_kernel(int E, int N, int C,
     const int r = child ? src - k : src;
     const uint8_t* s = (child ? cs : ps) + (long)r * E;
     const uint8_t* m = (child ? cr : pr) + (long)r * E;
-    for (int e = threadIdx.x; e < E; e += 64) {
-        ws[(long)i * E + e] = s[e];
-        wr[(long)i * E + e] = m[e];
-    }
+    copy_rows2(ws + (long)i * E, s, wr + (long)i * E, m, E, threadIdx.x);
     if (threadIdx.x == 0) {
         wm[4 * i + 0] = child ? ch[r] : ph[r];
         wm[4 * i + 1] = child ? csc[r] : psc[r];
@@ -402,10 +420,7 @@ __global__ __launch_bounds__(64) void replace_scatter_kernel(int E, const uint8_
                                                              int32_t* __restrict__ psc, uint8_t* __restrict__ pf,
                                                              int32_t* __restrict__ pp) {
     const int i = blockIdx.x;
-    for (int e = threadIdx.x; e < E; e += 64) {
-        ps[(long)i * E + e] = ws[(long)i * E + e];
-        pr[(long)i * E + e] = wr[(long)i * E + e];
-    }
+    copy_rows2(ps + (long)i * E, ws + (long)i * E, pr + (long)i * E, wr + (long)i * E, E, threadIdx.x);
     if (threadIdx.x == 0) {
         ph[i] = wm[4 * i + 0];
         psc[i] = wm[4 * i + 1];
