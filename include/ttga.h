@@ -46,8 +46,10 @@ typedef struct tt_problem tt_problem;
  * broadcast (ga.cpp:417-426): takes the parsed .tim matrices, derives
  * studentNumber (Problem.cpp:33-40), eventCorrelations (:42-58) and
  * possibleRooms (:76-95) exactly as the reference, and uploads the device
- * image to `device`. The derivation runs on the host in O(sum over students
- * of deg^2) instead of the reference's O(E^2 S) (timed in tools/time_problem.py).
+ * image to `device`. The derivation runs on the device: eventCorrelations =
+ * (A^T A > 0) as an int8 MFMA contraction over the students, studentNumber
+ * from its diagonal, possibleRooms in the same launch (csrc/tt_derive.hip);
+ * the host builds only the sparse (CSR) views of A. Synchronous.
  *   room_size[R], student_events[S*E] (row-major, 0/1), room_features[R*F],
  *   event_features[E*F] (0/1). */
 int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, const int32_t* student_events,
@@ -181,10 +183,13 @@ int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* pop_room, int
  *              (Solution.cpp:498-505,616-618) and the bound is twice that per
  *              phase; tests assert it never fires;
  *   bit 3 (8)  tt_local_search_ordered got a dispatch order that is not a
- *              permutation of 0..P-1 (an entry out of range, or a duplicate with
- *              an entry missing: checked on the device by range, sum and sum of
- *              squares); out-of-range entries are skipped, a duplicated
- *              individual is searched twice concurrently (undefined result).
+ *              permutation of 0..P-1 (an entry out of range, or an entry seen
+ *              twice: checked exactly on the device with a visited bitmap);
+ *              out-of-range entries are skipped, a duplicated individual is
+ *              searched twice concurrently (undefined result);
+ *   bit 4 (16) the local search's per-stream redo list overflowed (unreachable:
+ *              it holds P entries and a launch lists each wave at most once);
+ *              the individuals not listed are left unsearched.
  * Synchronises the device. */
 int tt_device_status(const tt_problem* p, int32_t* status);
 

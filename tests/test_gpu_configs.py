@@ -250,6 +250,36 @@ def test_islands_drivers_multiplexed_lg(tmp_path, orc):
     assert threads <= {0, 1}
 
 
+def test_rccl_one_rank_drivers_lg(tmp_path):
+    """The RCCL calls of both drivers on one GPU: `ttga-ga --rccl` (a one-rank
+    communicator from ncclCommInitAll: the population ncclBroadcast, the
+    migration's grouped ncclSend/ncclRecv pairs -- the ring neighbours are the
+    rank itself -- and the ncclAllReduce MIN) and `python -m ttga.islands
+    --force-dist` (an nccl process group at world 1: dist.broadcast,
+    batch_isend_irecv and all_reduce MIN) print the same JSON lines as the
+    device-copy paths on the lg instance through one migration (before
+    generation 49, ga.cpp:514-540); the printed timetables validate."""
+    inst = ttga.config_instance("lg")
+    tim = tmp_path / "lg.tim"
+    ttga.write_tim(inst, tim)
+    args = ["-i", str(tim), "-s", "11", "-p", "1", "-c", "4", "--pop", "16", "--generations", "54"]
+    exe = str(REPO / "timetabling-ga-mpi-openmp_amd" / "ttga-ga")
+    runs = {}
+    for name, cmd in (("cc", [exe, *args]), ("cc_rccl", [exe, *args, "--rccl"]),
+                      ("py", [sys.executable, "-m", "ttga.islands", *args]),
+                      ("py_dist", [sys.executable, "-m", "ttga.islands", *args, "--force-dist"])):
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=_env(), cwd=str(tmp_path))
+        assert p.returncode == 0, (name, p.stderr[-2000:])
+        runs[name] = p.stdout
+    lines = {k: _lines(v) for k, v in runs.items()}
+    assert sorted(lines["cc"][0]) == [0] and len(lines["cc"][0][0]) >= 2
+    for k in ("cc_rccl", "py", "py_dist"):
+        assert lines[k] == lines["cc"], k
+    from test_gpu_ga import assert_validated
+    for v in runs.values():
+        assert_validated(inst, tim, v)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -301,13 +301,19 @@ def test_best_thread_with_lpt_dispatch(sm):
 def test_local_search_order_permutation_check():
     """tt_local_search_ordered flags a dispatch order that is not a
     permutation (status bit 3): a duplicate entry (one individual missing), an
-    out-of-range entry; a true permutation leaves the status clean."""
+    out-of-range entry, three duplicates replacing {1, 5, 6} by {2, 3, 7}
+    (sum and sum of squares unchanged: only an exact check sees it); a true
+    permutation leaves the status clean."""
     inst = ttga.config_instance("med")
     P = 64
     seeds = ttga.population_seeds(31, P)
+    same_sums = np.arange(P)
+    same_sums[[1, 5, 6]] = [2, 3, 7]
+    assert same_sums.sum() == np.arange(P).sum() and (same_sums ** 2).sum() == (np.arange(P) ** 2).sum()
     for order, bad in ((np.random.default_rng(0).permutation(P), False),
                        (np.r_[np.arange(P - 1), 0], True),
-                       (np.r_[np.arange(P - 1), P], True)):
+                       (np.r_[np.arange(P - 1), P], True),
+                       (np.random.default_rng(1).permutation(same_sums), True)):
         dp = native.DeviceProblem(inst)
         s = dev(ttga.random_slots(seeds, inst.E)[0])
         r = dp.assign_rooms(s)

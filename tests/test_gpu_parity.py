@@ -327,6 +327,30 @@ def test_local_search_crowded_slots_redo(orc):
     assert dp.status() == 0
 
 
+def test_local_search_redo_list_reuse(orc):
+    """The per-stream redo list persists across calls: the redo launch resets
+    its count and arrival counter on the device, and a call with a larger
+    population regrows it. Three chained calls on one stream -- crowded
+    individuals at P = 12, again at P = 12, then at P = 40 (regrown) -- each
+    equal the oracle, with the status clean after every call."""
+    inst = ttga.generate(400, 10, 5, 200, seed=23)
+    dp = native.DeviceProblem(inst)
+    o = orc.problem(inst)
+    rng = np.random.default_rng(5)
+    for call, P in enumerate((12, 12, 40)):
+        s0, _, _ = o.random_init(ttga.population_seeds(1808 + call, P))
+        for k in range(1, P, 3):
+            idx = rng.choice(inst.E, size=int(rng.integers(65, 150)), replace=False)
+            s0[k, idx] = int(rng.integers(0, 45))           # one crowded slot
+        r0 = o.assign_rooms(s0)
+        seeds = ttga.population_seeds(1909 + call, P)
+        s, r, g = dev(s0), dev(r0), dev(seeds)
+        dp.local_search(s, r, g, 250)
+        es, er, eg = o.local_search(s0, r0, seeds, 250)
+        assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg), call
+        assert dp.status() == 0, call
+
+
 @pytest.mark.parametrize("p1,p2", [(1.0, 1.0), (0.7, 0.4)])
 def test_local_search_phase2_vs_oracle(orc, p1, p2):
     """Mostly-feasible individuals (3000 steps from random init), then a chained

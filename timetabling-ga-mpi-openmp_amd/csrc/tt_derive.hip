@@ -1,0 +1,203 @@
+// Problem derived data on the device (Problem.cpp:33-58,76-95), the f1 row of
+// eventCorrelations = (AᵀA > 0) as an int8 MFMA contraction over the
+// students, studentNumber from the diagonal of the same product, and
+// possibleRooms from it in the diagonal tiles' epilogue.
+//
+//   A   [S][E] u8 0/1 (student_events, student-major as the .tim holds it)
+//   At  [Ep][Sp] u8   event-major copy, Ep = E rounded up to 64, Sp = S rounded
+//                     up to 64, zero padded (derive_transpose_kernel)
+//   C = At · Atᵀ      C[i][j] = #students attending both i and j; C[i][i] =
+//                     studentNumber[i] since A is 0/1
+//
+// Mapping: one 4-wave workgroup per 64×64 block (bi <= bj) of C, one 32×32
+// quadrant per wave, v_mfma_i32_32x32x32_i8 over 32 students per step with
+// exact i32 accumulation. Both operands of a step are 16 consecutive students
+// of one event row per lane (a 16-B load): lane l holds row (l & 31) of its
+// operand tile at students 16·(l >> 5) .. +15, for A (events i) and for B
+// (events j) alike, so the k order is the same on both sides. C is symmetric,
+// so an off-diagonal block's quadrant is written twice: its rows (ballots of
+// C > 0 per accumulator register) and its columns (the bits of a lane's own
+// accumulators, the two lane halves OR-ed). The image parts written:
+//   corr  u32 [E][EW]       eventCorrelations rows (DevProblem::corr)
+//   corr64 u64 [E][EW64]    the same rows in 64-bit words
+//   cupT  u64 [EW64][E]     upper triangle, word-major (bits j > i)
+//   sn    i32 [E]           studentNumber
+//   poss  u64 [E]           possibleRooms bitmasks
+#include <hip/hip_runtime.h>
+
+#include "tt_internal.h"
+
+namespace ttga {
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// A [S][E] -> At [Ep][Sp], 64×64 byte tiles through LDS, zero padded.
+__global__ __launch_bounds__(256) void derive_transpose_kernel(const uint8_t* __restrict__ A, int S, int E,
+                                                               uint8_t* __restrict__ At, int Sp) {
+    __shared__ uint8_t tile[64][65];
+    const int s0 = blockIdx.x * 64, e0 = blockIdx.y * 64, t = threadIdx.x;
+    for (int k = t; k < 64 * 64; k += 256) {
+        const int s = s0 + (k >> 6), e = e0 + (k & 63);
+        tile[k >> 6][k & 63] = (s < S && e < E) ? A[(size_t)s * E + e] : (uint8_t)0;
+    }
+    __syncthreads();
+    // thread t: event row e0 + (t >> 2), 16 students at 16·(t & 3)
+    const int r = t >> 2, q = (t & 3) * 16;
+    v4i w;
+    uint32_t* wp = (uint32_t*)&w;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) x |= (uint32_t)tile[q + 4 * d + b][r] << (8 * b);
+        wp[d] = x;
+    }
+    *(v4i*)(At + (size_t)(e0 + r) * Sp + s0 + q) = w;
+}
+
+struct DeriveOut {
+    uint32_t* corr;     // [E][EW]
+    uint32_t* corr64;   // [E][2·EW64] as u32 words
+    uint32_t* cupT;     // [EW64][E] u64 as u32 pairs
+    int32_t* sn;        // [E]
+    uint64_t* poss;     // [E]
+};
+
+__device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+// Writes the 32-bit word of C-row i over columns j0 .. j0+31 to the three images.
+__device__ __forceinline__ void put_row_word(const DeriveOut& o, int E, int EW, int EW64, int i, int j0, uint32_t w) {
+    if (i >= E) return;
+    const int wd = j0 >> 5;
+    if (wd < EW) o.corr[(size_t)i * EW + wd] = w;
+    o.corr64[(size_t)i * (2 * EW64) + wd] = w;                   // wd < 2·EW64 always (j0 < Ep)
+    // upper triangle: bits j > i only
+    uint32_t up;
+    if (j0 > i) up = w;
+    else if (j0 + 31 <= i) up = 0u;
+    else up = w & ~((2u << (i - j0)) - 1u);                      // keep bits (i - j0 + 1) .. 31
+    o.cupT[((size_t)(j0 >> 6) * E + i) * 2 + (wd & 1)] = up;
+}
+
+__global__ __launch_bounds__(256) void derive_corr_kernel(const uint8_t* __restrict__ At, int E, int Sp, int nb,
+                                                          const int32_t* __restrict__ room_size, int R,
+                                                          const uint64_t* __restrict__ efw,
+                                                          const uint64_t* __restrict__ rfw, int FW, DeriveOut o) {
+    // block pair (bi <= bj) from the linear index, row-major over the upper triangle
+    int b = blockIdx.x, bi = 0;
+    while (b >= nb - bi) { b -= nb - bi; bi++; }
+    const int bj = bi + b;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int qi = w >> 1, qj = w & 1;
+    const bool diag_block = bi == bj;
+    if (diag_block && qi > qj) return;                         // the transpose of quadrant (0,1)
+    const int i0 = 64 * bi + 32 * qi, j0 = 64 * bj + 32 * qj;
+    const int r = lane & 31, h = lane >> 5;
+
+    const uint8_t* pa = At + (size_t)(i0 + r) * Sp + 16 * h;
+    const uint8_t* pb = At + (size_t)(j0 + r) * Sp + 16 * h;
+    v16i acc = {};
+    int s = 0;
+    for (; s + 128 <= Sp; s += 128) {                          // four steps, eight loads in flight
+        v4i a0 = *(const v4i*)(pa + s), b0 = *(const v4i*)(pb + s);
+        v4i a1 = *(const v4i*)(pa + s + 32), b1 = *(const v4i*)(pb + s + 32);
+        v4i a2 = *(const v4i*)(pa + s + 64), b2 = *(const v4i*)(pb + s + 64);
+        v4i a3 = *(const v4i*)(pa + s + 96), b3 = *(const v4i*)(pb + s + 96);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a2, b2, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a3, b3, acc, 0, 0, 0);
+    }
+    for (; s < Sp; s += 32) {
+        v4i a0 = *(const v4i*)(pa + s), b0 = *(const v4i*)(pb + s);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc, 0, 0, 0);
+    }
+
+    const int EW = (E + 31) >> 5, EW64 = (E + 63) >> 6;
+    // rows of the quadrant: accumulator register g holds row acc_row(g, h), column r
+    uint32_t myrow = 0u;                                       // lane t < 32: the word of row i0 + t
+    uint32_t colbits = 0u;                                     // this lane's column r over its 16 rows
+#pragma unroll
+    for (int g = 0; g < 16; g++) {
+        const bool nz = acc[g] > 0;
+        const uint64_t bal = ballot(nz);
+        // row acc_row(g, 0) is the low half, acc_row(g, 1) the high half
+        if (lane == acc_row(g, 0)) myrow = (uint32_t)bal;
+        if (lane == acc_row(g, 1)) myrow = (uint32_t)(bal >> 32);
+        if (nz) colbits |= 1u << acc_row(g, h);
+    }
+    const uint32_t col = colbits | (uint32_t)__shfl_xor((int)colbits, 32);
+    if (lane < 32) {
+        put_row_word(o, E, EW, EW64, i0 + lane, j0, myrow);
+        if (!(diag_block && qi == qj)) put_row_word(o, E, EW, EW64, j0 + lane, i0, col);   // C(j, i) rows
+    }
+    if (diag_block && qi == qj) {
+        // studentNumber from the diagonal: (row c, column c) sits in register
+        // (c & 3) + 4·(c >> 3) of the lane with column c and half (c >> 2) & 1
+        const int c = r;
+        if (h == ((c >> 2) & 1)) {
+            const int reg = (c & 3) + 4 * (c >> 3);
+            int v = 0;
+#pragma unroll
+            for (int g = 0; g < 16; g++) if (g == reg) v = acc[g];
+            const int e = i0 + c;
+            if (e < E) {
+                o.sn[e] = v;
+                // possibleRooms (Problem.cpp:76-95): size fits, every required feature present
+                uint64_t pm = 0ull;
+                for (int rr = 0; rr < R; rr++) {
+                    if (room_size[rr] < v) continue;
+                    bool ok = true;
+                    for (int f = 0; f < FW; f++) ok &= (efw[(size_t)e * FW + f] & ~rfw[(size_t)rr * FW + f]) == 0ull;
+                    if (ok) pm |= 1ull << rr;
+                }
+                o.poss[e] = pm;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+int derive_on_device(const tt_problem* p, const uint8_t* A_host, const int32_t* room_size, const uint64_t* efw,
+                     const uint64_t* rfw, int FW) {
+    const int E = p->E, S = p->S, R = p->R;
+    const int Ep = (E + 63) & ~63, Sp = (S + 63) & ~63, nb = Ep / 64;
+    const size_t a_bytes = ((size_t)S * E + 255) & ~(size_t)255, at_bytes = ((size_t)Ep * Sp + 255) & ~(size_t)255;
+    const size_t rs_bytes = 256 * ((sizeof(int32_t) * R + 255) / 256);
+    const size_t ef_bytes = ((sizeof(uint64_t) * E * FW) + 255) & ~(size_t)255;
+    const size_t rf_bytes = ((sizeof(uint64_t) * R * FW) + 255) & ~(size_t)255;
+    const size_t total = a_bytes + at_bytes + rs_bytes + ef_bytes + rf_bytes + 256;
+    uint8_t* tmp = nullptr;
+    hipStream_t st = nullptr;
+    TT_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    hipError_t he = hipMalloc(&tmp, total);
+    if (he != hipSuccess) { (void)hipStreamDestroy(st); return check_hip(he, "derive: hipMalloc"); }
+    uint8_t* dA = tmp;
+    uint8_t* dAt = dA + a_bytes;
+    int32_t* drs = (int32_t*)(dAt + at_bytes);
+    uint64_t* def = (uint64_t*)((uint8_t*)drs + rs_bytes);
+    uint64_t* drf = (uint64_t*)((uint8_t*)def + ef_bytes);
+    const DevProblem& d = p->dev;
+    DeriveOut o{const_cast<uint32_t*>(d.corr), (uint32_t*)const_cast<uint64_t*>(d.corr64),
+                (uint32_t*)const_cast<uint64_t*>(d.cupT), const_cast<int32_t*>(d.sn), const_cast<uint64_t*>(d.poss)};
+    if (S > 0) he = hipMemcpyAsync(dA, A_host, (size_t)S * E, hipMemcpyHostToDevice, st);
+    if (he == hipSuccess) he = hipMemcpyAsync(drs, room_size, sizeof(int32_t) * R, hipMemcpyHostToDevice, st);
+    if (he == hipSuccess && FW > 0) he = hipMemcpyAsync(def, efw, sizeof(uint64_t) * E * FW, hipMemcpyHostToDevice, st);
+    if (he == hipSuccess && FW > 0) he = hipMemcpyAsync(drf, rfw, sizeof(uint64_t) * R * FW, hipMemcpyHostToDevice, st);
+    if (he == hipSuccess && Sp > 0)
+        hipLaunchKernelGGL(derive_transpose_kernel, dim3(Sp / 64, Ep / 64), dim3(256), 0, st, dA, S, E, dAt, Sp);
+    if (he == hipSuccess) he = hipGetLastError();
+    if (he == hipSuccess)
+        hipLaunchKernelGGL(derive_corr_kernel, dim3(nb * (nb + 1) / 2), dim3(256), 0, st, dAt, E, Sp, nb, drs, R, def,
+                           drf, FW, o);
+    if (he == hipSuccess) he = hipGetLastError();
+    if (he == hipSuccess) he = hipStreamSynchronize(st);
+    (void)hipFree(tmp);
+    (void)hipStreamDestroy(st);
+    return check_hip(he, "derive_on_device");
+}
+
+}  // namespace ttga

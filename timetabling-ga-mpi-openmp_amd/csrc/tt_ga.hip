@@ -176,8 +176,9 @@ __global__ void bitonic_step_kernel(uint64_t* __restrict__ keys, int NP, int k, 
 // order, so the sorted merged population is the merge of them with the C
 // children's keys sorted on their own (one workgroup in LDS for C <= kSortTile).
 // Keys are unique (positions), so the merge equals the full sort. The survivors'
-// order is checked on the device; when it does not hold (the first call after
-// initialisation, a migration generation) a one-workgroup full sort runs instead.
+// order is checked on the device; when it does not hold (a migrant written into
+// pop[N-2] survives when C = 1) a one-workgroup full sort runs instead. C = 0
+// (the initial sort) takes the tiled sort directly.
 #ifndef TT_GA_MERGE
 #define TT_GA_MERGE 1
 #endif
@@ -566,7 +567,11 @@ extern "C" int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* po
     uint8_t* wr = ws + align256((size_t)N * E);
     int32_t* wm = (int32_t*)(wr + align256((size_t)N * E));
     const uint64_t* sorted = keys;
-    if (TT_GA_MERGE && C <= kSortTile) {
+    // C = 0 sorts a population with no order to rely on (the initial sort,
+    // ga.cpp:433-434): the multi-workgroup sort, not the merge path's
+    // one-workgroup fallback (which a generation meets only when a migrant
+    // survives out of order, C = 1)
+    if (TT_GA_MERGE && C > 0 && C <= kSortTile) {
         uint64_t* mkeys = (uint64_t*)(w + work_merge_offset(N, E));
         uint64_t* ckeys = (uint64_t*)((uint8_t*)mkeys + align256(8 * (size_t)N));
         int32_t* flag = (int32_t*)(ckeys + kSortTile);

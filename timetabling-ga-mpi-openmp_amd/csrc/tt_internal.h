@@ -16,7 +16,7 @@ struct tt_problem {
     std::vector<int32_t> student_number;
     std::vector<uint64_t> poss_bits;
     std::vector<uint32_t> corr_bits;
-    int nnz_students, nnz_pairs, max_cells;
+    int nnz_students;
     // device allocations
     void* dev_block;
     ttga::DevProblem dev;
@@ -54,5 +54,11 @@ int check_pop_args(const tt_problem* p, int P, const void* a, const void* b);
 
 // Makes the handle's device current for the calling thread.
 int use_device(const tt_problem* p);
+
+// studentNumber, eventCorrelations (corr, corr64, cupT) and possibleRooms of
+// the image, derived on the handle's (current) device from the u8 attendance
+// matrix A[S][E] (csrc/tt_derive.hip); synchronous.
+int derive_on_device(const tt_problem* p, const uint8_t* A, const int32_t* room_size, const uint64_t* efw,
+                     const uint64_t* rfw, int FW);
 
 }  // namespace ttga

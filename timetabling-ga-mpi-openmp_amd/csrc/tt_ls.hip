@@ -944,13 +944,14 @@ __device__ __forceinline__ int window_resolve(int lane, uint32_t jump, int64_t& 
 // One individual's localSearch by the calling wave (every lane). CAP =
 // matcher task capacity. redo_list (first launch, CAP = kLsCapSmall): an
 // individual that overflowed a task is appended to it (redo_list[0] counts,
-// entries from redo_list[2]) and its HBM row and stream are left as they
-// were; NULL when no task can overflow.
+// entries from redo_list[2], at most redo_cap of them: beyond that status bit
+// 4 is set) and its HBM row and stream are left as they were; NULL when no
+// task can overflow.
 template <int CAP>
 __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& pb, uint8_t* __restrict__ slot,
                                                              uint8_t* __restrict__ room, int64_t* __restrict__ rng,
                                                              long p, int max_steps, double p1, double p2, double p3,
-                                                             int32_t* __restrict__ redo_list, int smS) {
+                                                             int32_t* __restrict__ redo_list, int redo_cap, int smS) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int E = pb.E, R = pb.R, EW = pb.EW64;
     const int lane = threadIdx.x;
@@ -1485,7 +1486,11 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
 #endif
     return;
 redo:
-    if (lane == 0) redo_list[2 + atomicAdd(&redo_list[0], 1)] = (int32_t)p;
+    if (lane == 0) {
+        const int k = atomicAdd(&redo_list[0], 1);
+        if (k < redo_cap) redo_list[2 + k] = (int32_t)p;
+        else atomicOr(pb.status, 16);
+    }
 }
 
 #ifndef TT_LS_WPE
@@ -1497,11 +1502,11 @@ redo:
 template <int CAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE))) void local_search_kernel(
     DevProblem pb, uint8_t* __restrict__ slot, uint8_t* __restrict__ room, int64_t* __restrict__ rng, int P,
-    int max_steps, double p1, double p2, double p3, int32_t* __restrict__ redo_list, const int32_t* __restrict__ order,
-    int smS) {
+    int max_steps, double p1, double p2, double p3, int32_t* __restrict__ redo_list, int redo_cap,
+    const int32_t* __restrict__ order, int smS) {
     const long p = order ? (long)order[blockIdx.x] : (long)blockIdx.x;   // dispatch order only
     if ((unsigned long)p >= (unsigned long)P) return;
-    ls_one<CAP>(pb, slot, room, rng, p, max_steps, p1, p2, p3, redo_list, smS);
+    ls_one<CAP>(pb, slot, room, rng, p, max_steps, p1, p2, p3, redo_list, redo_cap, smS);
 }
 
 // Redo launch: a grid of resident waves works through the individuals the
@@ -1511,12 +1516,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE)))
 // there is a list to reset: 52 -> a few us per GA generation).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE))) void local_search_redo_kernel(
     DevProblem pb, uint8_t* __restrict__ slot, uint8_t* __restrict__ room, int64_t* __restrict__ rng, int max_steps,
-    double p1, double p2, double p3, int32_t* __restrict__ redo_list, int smS) {
-    const int n = redo_list[0];
+    double p1, double p2, double p3, int32_t* __restrict__ redo_list, int redo_cap, int smS) {
+    const int n = min(redo_list[0], redo_cap);
     if (n == 0) return;             // nothing listed: every wave sees 0, no reset needed (no arrival atomics)
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         __syncthreads();
-        ls_one<kMaxSlotEvents>(pb, slot, room, rng, (long)redo_list[2 + i], max_steps, p1, p2, p3, nullptr, smS);
+        ls_one<kMaxSlotEvents>(pb, slot, room, rng, (long)redo_list[2 + i], max_steps, p1, p2, p3, nullptr, 0, smS);
     }
     __threadfence();
     if (threadIdx.x == 0 && atomicAdd(&redo_list[1], 1) == (int)gridDim.x - 1) {
@@ -1525,37 +1530,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE)))
     }
 }
 
-// Permutation check of a dispatch order (status bit 3 when it is not one):
-// every entry in 0..P-1, and the sum and the sum of squares (mod 2^64) equal
-// those of 0..P-1 -- a duplicate with a missing entry changes the sum.
-__global__ __launch_bounds__(1024) void order_check_kernel(const int32_t* __restrict__ order, int P,
+// Permutation check of a dispatch order (status bit 3 when it is not one),
+// exact: every entry in 0..P-1 and none seen twice (P entries in range with no
+// duplicate are a permutation). One workgroup marks the entries in a visited
+// bitmap in LDS, `bits` entries per pass (every pass reads the whole order).
+__global__ __launch_bounds__(1024) void order_check_kernel(const int32_t* __restrict__ order, int P, int bits,
                                                            int32_t* __restrict__ status) {
-    __shared__ unsigned long long red[2][16];
+    extern __shared__ uint32_t seen[];
     __shared__ int bad_any;
     if (threadIdx.x == 0) bad_any = 0;
-    __syncthreads();
-    unsigned long long s1 = 0, s2 = 0;
     bool bad = false;
-    for (int i = threadIdx.x; i < P; i += 1024) {
-        const int v = order[i];
-        bad |= v < 0 || v >= P;
-        const unsigned long long d = (unsigned long long)(unsigned)v - (unsigned long long)(unsigned)i;
-        const unsigned long long q = (unsigned long long)(unsigned)v * (unsigned)v - (unsigned long long)(unsigned)i * (unsigned)i;
-        s1 += d;
-        s2 += q;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        s1 += __shfl_down(s1, o);
-        s2 += __shfl_down(s2, o);
+    for (int lo = 0; lo < P; lo += bits) {
+        const int hi = min(P, lo + bits);
+        for (int w = threadIdx.x; w < (hi - lo + 31) / 32; w += 1024) seen[w] = 0u;
+        __syncthreads();
+        for (int i = threadIdx.x; i < P; i += 1024) {
+            const int v = order[i];
+            if (lo == 0) bad |= v < 0 || v >= P;
+            if (v >= lo && v < hi) {
+                const uint32_t bit = 1u << ((v - lo) & 31);
+                bad |= (atomicOr(&seen[(v - lo) >> 5], bit) & bit) != 0u;
+            }
+        }
+        __syncthreads();
     }
     if (bad) atomicOr(&bad_any, 1);
-    if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = s1; red[1][threadIdx.x >> 6] = s2; }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long a = 0, b = 0;
-        for (int w = 0; w < 16; ++w) { a += red[0][w]; b += red[1][w]; }
-        if (bad_any || a || b) atomicOr(status, 8);
-    }
+    if (threadIdx.x == 0 && bad_any) atomicOr(status, 8);
 }
 
 }  // namespace ttga
@@ -1605,6 +1606,9 @@ static int ls_mask_students(const tt_problem* p, int cap, K k, int P) {
     return (o1 >= o0 || per_cu <= o1) ? p->dev.S : 0;
 }
 
+// entries of a dispatch order checked per pass of order_check_kernel (128 KB of LDS)
+constexpr int kOrderCheckBits = 128 * 1024 * 8;
+
 extern "C" int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P,
                                int max_steps, double p1, double p2, double p3, void* stream) {
     return tt_local_search_ordered(p, slot, room, rng, P, max_steps, p1, p2, p3, nullptr, stream);
@@ -1623,12 +1627,14 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
     if (Lf.bytes > 160 * 1024) { set_error("instance too large for the local-search kernel"); return TT_ERR_LIMIT; }
     hipStream_t st = (hipStream_t)stream;
     if (order) {
-        hipLaunchKernelGGL(order_check_kernel, dim3(1), dim3(1024), 0, st, order, P, p->dev.status);
+        const int bits = std::min(P, kOrderCheckBits);
+        hipLaunchKernelGGL(order_check_kernel, dim3(1), dim3(1024), sizeof(uint32_t) * ((bits + 31) / 32), st, order, P,
+                           bits, p->dev.status);
         TT_HIP(hipGetLastError());
     }
     if (p->E <= kLsCapSmall) {                      // no slot can exceed the small tasks
         hipLaunchKernelGGL(local_search_kernel<kMaxSlotEvents>, dim3(P), dim3(64), Lf.bytes, st, p->dev, slot, room,
-                           rng, P, max_steps, p1, p2, p3, (int32_t*)nullptr, order, smf);
+                           rng, P, max_steps, p1, p2, p3, (int32_t*)nullptr, 0, order, smf);
         return check_hip(hipGetLastError(), "local_search launch");
     }
     const int sms = ls_mask_students(p, kLsCapSmall, local_search_kernel<kLsCapSmall>, P);
@@ -1652,14 +1658,21 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
         rl->cap = P;
     }
     hipLaunchKernelGGL(local_search_kernel<kLsCapSmall>, dim3(P), dim3(64), Ls.bytes, st, p->dev, slot, room, rng, P,
-                       max_steps, p1, p2, p3, rl->list, order, sms);
+                       max_steps, p1, p2, p3, rl->list, rl->cap, order, sms);
     TT_HIP(hipGetLastError());
     // the redo launch: resident waves only (an empty list costs one short launch)
     int per_cu = 0;
-    TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, local_search_redo_kernel, 64, Lf.bytes));
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, local_search_redo_kernel, 64, Lf.bytes) != hipSuccess)
+        per_cu = 1;
     const int grid = std::min(P, std::max(1, per_cu) * p->num_cus);
     hipLaunchKernelGGL(local_search_redo_kernel, dim3(grid), dim3(64), Lf.bytes, st, p->dev, slot, room, rng,
-                       max_steps, p1, p2, p3, rl->list, smf);
-    TT_HIP(hipGetLastError());
+                       max_steps, p1, p2, p3, rl->list, rl->cap, smf);
+    const hipError_t he = hipGetLastError();
+    if (he != hipSuccess) {
+        // the first launch may have listed individuals: leave the list empty
+        // for the stream's next call instead of redoing stale entries
+        (void)hipMemsetAsync(rl->list, 0, sizeof(int32_t) * 2, st);
+        return check_hip(he, "local_search redo launch");
+    }
     return TT_OK;
 }

@@ -54,60 +54,50 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         set_error("null instance matrix");
         return TT_ERR_INVALID;
     }
-    for (long i = 0; i < (long)S * E; i++)
-        if (A[i] != 0 && A[i] != 1) { set_error("student_events must be 0/1"); return TT_ERR_INVALID; }
     for (long i = 0; i < (long)R * F; i++)
         if (room_feat[i] != 0 && room_feat[i] != 1) { set_error("room_features must be 0/1"); return TT_ERR_INVALID; }
     for (long i = 0; i < (long)E * F; i++)
         if (event_feat[i] != 0 && event_feat[i] != 1) { set_error("event_features must be 0/1"); return TT_ERR_INVALID; }
 
+    // One pass over student_events: the 0/1 check, the u8 copy the device
+    // derivation uploads, and the two CSR views (the students' events and the
+    // events' students) that the kernels read. The event degrees of the CSR are
+    // studentNumber; the device derives it again from the diagonal of AᵀA and
+    // the two must agree (checked below).
+    std::vector<uint8_t> a8((size_t)S * E);
+    std::vector<int32_t> stu_off(S + 1, 0), stu_ev, ev_off(E + 1, 0), ev_stu, degree(E, 0);
+    for (int s = 0; s < S; s++) {
+        const int32_t* row = A + (size_t)s * E;
+        uint8_t* out8 = a8.data() + (size_t)s * E;
+        int32_t bad = 0;
+        for (int e = 0; e < E; e++) { bad |= row[e] & ~1; out8[e] = (uint8_t)row[e]; }
+        if (bad) { set_error("student_events must be 0/1"); return TT_ERR_INVALID; }
+        for (int e = 0; e < E; e++)
+            if (out8[e]) { stu_ev.push_back(e); degree[e]++; }
+        stu_off[s + 1] = (int32_t)stu_ev.size();
+    }
+
     tt_problem* p = new tt_problem();
     p->E = E; p->R = R; p->F = F; p->S = S; p->device = device;
     const int EW = (E + 31) / 32;
+    const int EW64 = (E + 63) / 64;
 
-    // studentNumber (Problem.cpp:33-40) and the two CSR views of student_events.
-    std::vector<int32_t> stu_off(S + 1, 0), stu_ev, ev_off(E + 1, 0), ev_stu;
-    p->student_number.assign(E, 0);
-    for (int s = 0; s < S; s++) {
-        for (int e = 0; e < E; e++)
-            if (A[(long)s * E + e]) { stu_ev.push_back(e); p->student_number[e]++; }
-        stu_off[s + 1] = (int32_t)stu_ev.size();
-    }
-    for (int e = 0; e < E; e++) ev_off[e + 1] = ev_off[e] + p->student_number[e];
+    for (int e = 0; e < E; e++) ev_off[e + 1] = ev_off[e] + degree[e];
     ev_stu.resize(stu_ev.size());
     {
         std::vector<int32_t> cur(ev_off.begin(), ev_off.end() - 1);
         for (int s = 0; s < S; s++)
             for (int k = stu_off[s]; k < stu_off[s + 1]; k++) ev_stu[cur[stu_ev[k]]++] = s;
     }
-    // eventCorrelations (Problem.cpp:42-58): i ~ j iff a student attends both
-    // (diagonal set for events with students). Built student-major.
-    p->corr_bits.assign((size_t)E * EW, 0u);
-    for (int s = 0; s < S; s++)
-        for (int a = stu_off[s]; a < stu_off[s + 1]; a++)
-            for (int b = stu_off[s]; b < stu_off[s + 1]; b++) {
-                int i = stu_ev[a], j = stu_ev[b];
-                p->corr_bits[(size_t)i * EW + (j >> 5)] |= 1u << (j & 31);
-            }
-    std::vector<int32_t> cp_off(E + 1, 0), cp_j;
-    for (int i = 0; i < E; i++) {
-        for (int j = i + 1; j < E; j++)
-            if (p->corr_bits[(size_t)i * EW + (j >> 5)] >> (j & 31) & 1u) cp_j.push_back(j);
-        cp_off[i + 1] = (int32_t)cp_j.size();
-    }
-    // word-major upper-triangle correlation bits for the bitset hcv term, and
-    // 8-padded per-student lists for the lane-per-individual attendance masks
-    const int EW64 = (E + 63) / 64;
-    std::vector<uint64_t> cupT((size_t)EW64 * E, 0ull);
-    for (int i = 0; i < E; i++)
-        for (int k = cp_off[i]; k < cp_off[i + 1]; k++) {
-            const int j = cp_j[k];
-            cupT[(size_t)(j >> 6) * E + i] |= 1ull << (j & 63);
-        }
-    std::vector<uint64_t> corr64((size_t)E * EW64, 0ull);
-    for (int i = 0; i < E; i++)
-        for (int j = 0; j < E; j++)
-            if (p->corr_bits[(size_t)i * EW + (j >> 5)] >> (j & 31) & 1u) corr64[(size_t)i * EW64 + (j >> 6)] |= 1ull << (j & 63);
+    // features as bit words for the device's possibleRooms test
+    const int FW = (F + 63) / 64;
+    std::vector<uint64_t> efw((size_t)E * FW, 0ull), rfw((size_t)R * FW, 0ull);
+    for (int e = 0; e < E; e++)
+        for (int f = 0; f < F; f++)
+            if (event_feat[(size_t)e * F + f]) efw[(size_t)e * FW + (f >> 6)] |= 1ull << (f & 63);
+    for (int r = 0; r < R; r++)
+        for (int f = 0; f < F; f++)
+            if (room_feat[(size_t)r * F + f]) rfw[(size_t)r * FW + (f >> 6)] |= 1ull << (f & 63);
     std::vector<int32_t> stc_off(S + 1, 0), stc_ev;
     for (int s = 0; s < S; s++) {
         for (int k = stu_off[s]; k < stu_off[s + 1]; k++) stc_ev.push_back(stu_ev[k]);
@@ -163,34 +153,23 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     }
     sid.resize(sid.size() + 32, (uint16_t)E);             // slack for 64-B scalar over-reads
     if (srun_flat.empty()) srun_flat.assign(4, 0);
-    // possibleRooms (Problem.cpp:76-95): size fits and every required feature present.
-    p->poss_bits.assign(E, 0ull);
-    for (int i = 0; i < E; i++)
-        for (int j = 0; j < R; j++) {
-            if (room_size[j] < p->student_number[i]) continue;
-            bool ok = true;
-            for (int k = 0; k < F && ok; k++)
-                if (event_feat[(long)i * F + k] == 1 && room_feat[(long)j * F + k] == 0) ok = false;
-            if (ok) p->poss_bits[i] |= 1ull << j;
-        }
     p->nnz_students = (int)stu_ev.size();
-    p->nnz_pairs = (int)cp_j.size();
 
     // One device block, 256-B aligned sub-buffers.
     struct Part { const void* src; size_t bytes; size_t off; };
     std::vector<Part> parts = {
-        {p->student_number.data(), sizeof(int32_t) * E, 0},
+        {nullptr, sizeof(int32_t) * E, 0},                      // studentNumber (device-derived)
         {stu_off.data(), sizeof(int32_t) * (S + 1), 0},
         {stu_ev.data(), sizeof(int32_t) * stu_ev.size(), 0},
         {ev_off.data(), sizeof(int32_t) * (E + 1), 0},
         {ev_stu.data(), sizeof(int32_t) * ev_stu.size(), 0},
-        {p->poss_bits.data(), sizeof(uint64_t) * E, 0},
-        {p->corr_bits.data(), sizeof(uint32_t) * p->corr_bits.size(), 0},
+        {nullptr, sizeof(uint64_t) * E, 0},                     // possibleRooms (device-derived)
+        {nullptr, sizeof(uint32_t) * E * EW, 0},                // eventCorrelations (device-derived)
         {nullptr, sizeof(int32_t) * 4, 0},   // status word
-        {cupT.data(), sizeof(uint64_t) * cupT.size(), 0},
+        {nullptr, sizeof(uint64_t) * EW64 * E, 0},              // cupT (device-derived)
         {stc_off.data(), sizeof(int32_t) * stc_off.size(), 0},
         {stc_ev.data(), sizeof(int32_t) * stc_ev.size(), 0},
-        {corr64.data(), sizeof(uint64_t) * corr64.size(), 0},
+        {nullptr, sizeof(uint64_t) * E * EW64, 0},              // corr64 (device-derived)
         {sid.data(), sizeof(uint16_t) * sid.size(), 0},
         {srun_flat.data(), sizeof(int32_t) * srun_flat.size(), 0},
         {srun_part.data(), sizeof(int32_t) * srun_part.size(), 0},
@@ -210,7 +189,6 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
         if (q.src && q.bytes) memcpy(staging.data() + q.off, q.src, q.bytes);
     he = hipMemcpy(p->dev_block, staging.data(), total, hipMemcpyHostToDevice);
     if (he != hipSuccess) { check_hip(he, "tt_problem_create upload"); (void)hipFree(p->dev_block); delete p; return TT_ERR_DEVICE; }
-    (void)hipSetDevice(prev);
 
     uint8_t* base = (uint8_t*)p->dev_block;
     DevProblem& d = p->dev;
@@ -231,6 +209,30 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     d.sid = (const uint32_t*)(base + parts[12].off);
     d.srun = (const int4*)(base + parts[13].off);
     d.srun_part = (const int32_t*)(base + parts[14].off);
+
+    // studentNumber, eventCorrelations (and its two other layouts) and
+    // possibleRooms: the MFMA derivation (csrc/tt_derive.hip)
+    int rc = TT_OK;
+    he = hipSetDevice(device);
+    if (he != hipSuccess) rc = check_hip(he, "tt_problem_create");
+    if (rc == TT_OK) rc = derive_on_device(p, a8.data(), room_size, efw.data(), rfw.data(), FW);
+    // host copies for tt_problem_derived and the kernels' launch choices
+    p->student_number.assign(E, 0);
+    p->poss_bits.assign(E, 0ull);
+    p->corr_bits.assign((size_t)E * EW, 0u);
+    if (rc == TT_OK) rc = check_hip(hipMemcpy(p->student_number.data(), d.sn, sizeof(int32_t) * E, hipMemcpyDeviceToHost), "tt_problem_create readback");
+    if (rc == TT_OK) rc = check_hip(hipMemcpy(p->poss_bits.data(), d.poss, sizeof(uint64_t) * E, hipMemcpyDeviceToHost), "tt_problem_create readback");
+    if (rc == TT_OK) rc = check_hip(hipMemcpy(p->corr_bits.data(), d.corr, sizeof(uint32_t) * E * EW, hipMemcpyDeviceToHost), "tt_problem_create readback");
+    if (rc == TT_OK && p->student_number != degree) {
+        set_error("tt_problem_create: device studentNumber differs from the attendance counts");
+        rc = TT_ERR_DEVICE;
+    }
+    (void)hipSetDevice(prev);
+    if (rc != TT_OK) {
+        (void)hipFree(p->dev_block);
+        delete p;
+        return rc;
+    }
     *out = p;
     return TT_OK;
 }

@@ -4,10 +4,13 @@
 // communicator rank per GPU, ncclCommInitAll), the OpenMP threads of a rank
 // become C children bred per batched generation. With --islands K != --gpus,
 // island g runs on GPU g % gpus and migrants move by device copies (the same
-// ring, no communicator): K islands can share one GPU.
+// ring, no communicator): K islands can share one GPU. --rccl takes the RCCL
+// path for one island on one GPU too (a one-rank communicator: the ring's
+// send/recv pairs go to the rank itself), so the communicator's calls run on a
+// one-GPU box.
 //
 //   ttga-ga -i instance.tim [-s seed] [-p type] [-c children]
-//           [-p1 x -p2 y -p3 z] [--gpus G] [--islands K] [--pop N] [--generations n]
+//           [-p1 x -p2 y -p3 z] [--gpus G] [--islands K] [--pop N] [--generations n] [--rccl]
 //
 // Reference correspondence:
 //  * CLI: `-key value` pairs and messages of Control::Control (Control.cpp:3-137);
@@ -78,12 +81,17 @@ struct Control {
     long seed = 0;
     std::string input, output;
     int gpus = 1, islands = 0, pop = 10, generations = -1;
+    bool rccl = false;
 };
 
 // Control::Control (Control.cpp:3-137) plus the --gpus/--pop/--generations extensions.
 Control parse_control(int argc, char** argv) {
     std::vector<std::string> args(argv + 1, argv + argc);
     Control c;
+    if (auto it = std::find(args.begin(), args.end(), "--rccl"); it != args.end()) {
+        c.rccl = true;
+        args.erase(it);
+    }
     for (const char* k : {"--gpus", "--islands", "--pop", "--generations", "--children"}) {
         auto it = std::find(args.begin(), args.end(), k);
         if (it != args.end()) {
@@ -553,7 +561,8 @@ int main(int argc, char** argv) {
     const int N = ctl.pop;
     const int C = std::max(1, std::min(ctl.threads, N));
     const int gens = ctl.generations >= 0 ? ctl.generations : (2001 + C - 1) / C;   // generations 0..2000 (ga.cpp:510)
-    const bool rccl = K == G && K > 1;           // one island per GPU: RCCL ring; otherwise device copies
+    if (ctl.rccl && K != G) die("--rccl needs one island per GPU (--islands equal to --gpus)");
+    const bool rccl = K == G && (K > 1 || ctl.rccl);   // one island per GPU: RCCL ring; otherwise device copies
 
     std::vector<Island> isl(K);
     for (int k = 0; k < K; k++) {
@@ -652,21 +661,21 @@ int main(int argc, char** argv) {
     long gmin = *std::min_element(best_value.begin(), best_value.end());
     if (rccl) {
         std::vector<std::thread> red;
-        std::vector<int32_t*> dv(K, nullptr);
+        std::vector<int64_t*> dv(K, nullptr);        // hcv * 1e6 + scv can pass 2^31
         for (int k = 0; k < K; k++)
             red.emplace_back([&, k] {
                 Island& I = isl[k];
                 check_hip(hipSetDevice(I.device), "hipSetDevice");
                 check_hip(hipMalloc(&dv[k], 8), "hipMalloc");
-                const int32_t v = (int32_t)best_value[k];
-                check_hip(hipMemcpy(dv[k], &v, 4, hipMemcpyHostToDevice), "hipMemcpy");
-                check_nccl(ncclAllReduce(dv[k], dv[k], 1, ncclInt32, ncclMin, comms[k], I.st), "ncclAllReduce");
+                const int64_t v = best_value[k];
+                check_hip(hipMemcpy(dv[k], &v, 8, hipMemcpyHostToDevice), "hipMemcpy");
+                check_nccl(ncclAllReduce(dv[k], dv[k], 1, ncclInt64, ncclMin, comms[k], I.st), "ncclAllReduce");
                 check_hip(hipStreamSynchronize(I.st), "hipStreamSynchronize");
             });
         for (auto& t : red) t.join();
-        int32_t v = 0;
+        int64_t v = 0;
         check_hip(hipSetDevice(0), "hipSetDevice");
-        check_hip(hipMemcpy(&v, dv[0], 4, hipMemcpyDeviceToHost), "hipMemcpy");
+        check_hip(hipMemcpy(&v, dv[0], 8, hipMemcpyDeviceToHost), "hipMemcpy");
         gmin = v;
         for (int k = 0; k < K; k++) { (void)hipSetDevice(k); (void)hipFree(dv[k]); }
     }

@@ -13,7 +13,10 @@ Reference correspondence:
   children bred per generation. Extensions: `--pop N` (ga.cpp:64 has 10,
   N >= 3), `--islands K` (islands per process, default 1), `--generations G`,
   `--backend nccl|gloo` (gloo stages migrants through host memory; with it
-  several ranks may share one GPU).
+  several ranks may share one GPU), `--force-dist` (initialise the process
+  group and route the broadcast, the ring send/recv pairs and the MIN through
+  torch.distributed even at world 1: a one-rank RCCL communicator whose ring
+  neighbours are the rank itself, so the RCCL calls run on a one-GPU box).
 * islands: island g = rank*K + k of W = world*K; seed abs(seed + g*(seed/10))
   (ga.cpp:410-415), the base seed chosen by rank 0 (time(NULL) when -s is
   missing, ga.cpp:401) and broadcast; procID = g.
@@ -98,6 +101,13 @@ def parse_control(argv, out=sys.stdout, err=sys.stderr) -> dict:
     return c
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def rank_seed(seed: int, rank: int) -> int:
     """ga.cpp:412 with C int division."""
     q = abs(seed) // 10
@@ -120,7 +130,7 @@ def _exchange(send, dst: int, src: int, backend: str):
     return got
 
 
-def ring_migrate(islands, rank: int, world: int, backend: str = "nccl"):
+def ring_migrate(islands, rank: int, world: int, backend: str = "nccl", use_dist: bool | None = None):
     """ga.cpp:514-540 with one migrant each way over the ring of all W =
     world * K islands (island g = rank * K + k): g's best replaces pop[N-1] of
     island (g+1) % W, g's 2nd best replaces pop[N-2] of island (g-1) % W. All
@@ -133,7 +143,7 @@ def ring_migrate(islands, rank: int, world: int, backend: str = "nccl"):
         raise ValueError("ring migration needs a population of at least 3")
     best = [isl.pack(0) for isl in islands]
     second = [isl.pack(1) for isl in islands]
-    if world == 1:
+    if not (world > 1 if use_dist is None else use_dist):
         from_left, from_right = best[-1], second[0]
     else:
         right, left = (rank + 1) % world, (rank - 1 + world) % world
@@ -144,30 +154,30 @@ def ring_migrate(islands, rank: int, world: int, backend: str = "nccl"):
         isl.unpack_into(N - 2, second[k + 1] if k < K - 1 else from_right)
 
 
-def global_min(value: int, device, world: int, backend: str = "nccl") -> int:
+def global_min(value: int, device, world: int, backend: str = "nccl", use_dist: bool | None = None) -> int:
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if not (world > 1 if use_dist is None else use_dist):
         return int(value)
     t = torch.tensor([int(value)], dtype=torch.int64, device=device if backend != "gloo" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return int(t.item())
 
 
-def share_seed(seed, world: int) -> int:
+def share_seed(seed, world: int, use_dist: bool | None = None) -> int:
     """Rank 0's base seed on every rank (ga.cpp:401,410-415)."""
     import torch.distributed as dist
-    if world == 1:
+    if not (world > 1 if use_dist is None else use_dist):
         return int(seed)
     lst = [int(seed)]
     dist.broadcast_object_list(lst, src=0)
     return int(lst[0])
 
 
-def broadcast_population(islands, world: int, backend: str = "nccl"):
+def broadcast_population(islands, world: int, backend: str = "nccl", use_dist: bool | None = None):
     """Island 0 of rank 0 to every island (ga.cpp:436-444,461-464)."""
     import torch.distributed as dist
-    if world > 1:
+    if world > 1 if use_dist is None else use_dist:
         for t in islands[0].pop.values():
             if backend == "gloo" and t.is_cuda:
                 h = t.cpu()
@@ -198,9 +208,17 @@ def main(argv=None):
         i = argv.index("--backend")
         backend = argv[i + 1]
         argv = argv[:i] + argv[i + 2:]
+    use_dist = world > 1
+    if "--force-dist" in argv:
+        use_dist = True
+        argv = [a for a in argv if a != "--force-dist"]
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("WORLD_SIZE", str(world))
+        os.environ.setdefault("RANK", str(rank))
     device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
-    if world > 1:
+    if use_dist:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
@@ -208,7 +226,7 @@ def main(argv=None):
     ctl = parse_control(argv, out=sys.stdout if rank == 0 else open(os.devnull, "w"),
                         err=sys.stderr if rank == 0 else open(os.devnull, "w"))
     out = sys.stdout                 # ga.cpp:60: -o is parsed, output always goes to cout
-    seed = share_seed(ctl["seed"], world)
+    seed = share_seed(ctl["seed"], world, use_dist)
     inst = tim.read_tim(ctl["input"])
     dp = DeviceProblem(inst, device=device)
     C = ctl.get("children", ctl["threads"])
@@ -224,7 +242,7 @@ def main(argv=None):
                for k in range(K)]
     if rank == 0:
         islands[0].initialize()
-    broadcast_population(islands, world, backend)
+    broadcast_population(islands, world, backend, use_dist)
     torch.cuda.synchronize()
     t_begin = time.perf_counter()    # beginTry (ga.cpp:476)
     logs = [CostLog(rank * K + k, out, t_begin) for k in range(K)]
@@ -233,27 +251,27 @@ def main(argv=None):
     gens = ctl.get("generations", math.ceil(TOTAL_CHILDREN / C))
     for g in range(gens):
         if (g + 1) % 100 == 50:
-            if world > 1:
+            if use_dist:
                 dist.barrier()
-            ring_migrate(islands, rank, world, backend)
+            ring_migrate(islands, rank, world, backend, use_dist)
         for log, isl in zip(logs, islands):
             isl.step()
             log.update(isl, isl.best_thread())
     torch.cuda.synchronize()
     vals = [isl.best_value() for isl in islands]
-    gmin = global_min(min(v for _, v in vals), torch.device("cuda", device), world, backend)
+    gmin = global_min(min(v for _, v in vals), torch.device("cuda", device), world, backend, use_dist)
     if rank == 0:
         # setGlobalCost: "feasible" is rank 0's own pop[0] (ga.cpp:236-256)
         out.write(run_best_line(vals[0][0], gmin) + "\n")
     for k, isl in enumerate(islands):
         out.write(solution_line(isl.member(0), rank * K + k, time.perf_counter() - t_begin) + "\n")
     out.flush()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     if rank == 0:
         out.write(run_final_line(W, C, time.perf_counter() - t_start) + "\n")
     out.flush()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

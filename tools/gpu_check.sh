@@ -2,11 +2,15 @@
 # GPU checks for one gpurun call. Each step runs under its own time limit and
 # the script stops at the first timeout / abort / crash (exit >= 124); test
 # failures (exit 1) do not stop the later measurement steps.
-# usage: tools/gpu_check.sh [tag] [steps...]   steps: tests smoke bench prof
+# usage: tools/gpu_check.sh [tag] [steps...]
+#   tests gatests derive smoke bench prof benchsyn profsyn benchlg phases quality
+#   ls ls1000 ga8k ga32k gatrace lsprof timeprob profderive pmcderive listpmc
+#   pmc1..pmc4 (headline eval) pmcls (phase-2 local search) pmcga (GA children's
+#   local search) pmcwide (syn wide path) abls abeval
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-TAG=${1:-r01}; shift || true
+TAG=${1:-r04}; shift || true
 STEPS=${*:-tests smoke bench prof}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
@@ -16,14 +20,33 @@ run() {
     timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
     local rc=$?
     echo "== $name rc=$rc"
-    tail -n 5 "$OUT/$name.log"
+    tail -c 700 "$OUT/$name.log"; echo
     if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
     return 0
 }
+# PMC passes of one command, each pass its own run (rocprofv3 does not split
+# counters over passes); summary by tools/pmc_summary.py for kernel $2
+PASS1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS"
+PASS2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH GRBM_GUI_ACTIVE"
+PASS3="SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU"
+pmc() {
+    local name=$1 kernel=$2; shift 2
+    local i=0 c
+    for c in "$PASS1" "$PASS2" "$PASS3"; do
+        i=$((i + 1))
+        echo "== $name pass $i"
+        timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d "$OUT/$name/pmc$i" -o pmc -- "$@" \
+            > "$OUT/$name.pmc$i.log" 2>&1 || { echo "pmc pass $i rc=$?"; exit 125; }
+    done
+    python tools/pmc_summary.py "$OUT/$name" "$kernel" > "$OUT/$name.json"; cat "$OUT/$name.json"
+}
+GA8K="--config comp01 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6"
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
+    tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     gatests) run pytest_ga 600 python -u -m pytest tests/test_gpu_ga.py -m gpu -v --timeout 300 --timeout-method thread ;;
+    derive) run pytest_derive 400 python -u -m pytest tests/test_gpu_derive.py -m gpu -v --timeout 200 --timeout-method thread ;;
+    newtests) run pytest_new 600 python -u -m pytest tests/test_gpu_derive.py tests/test_gpu_ga.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread -k "derive or derived or permutation or redo" ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py ;;
     benchsyn) run bench_syn 600 python -u bench.py --config syn --pop 262144 --steps 10 --warmup 2 ;;
@@ -31,14 +54,27 @@ for s in $STEPS; do
     benchlg) run bench_lg 600 python -u bench.py --config lg --steps 100 ;;
     phases) run phases 300 python -u tools/eval_variants.py med 65536 8,24,40,72,136,264,520 ;;
     quality) run ga_quality 900 python -u tools/ga_quality.py --config sm --seeds 16 --gens 2001 --steps 200 --out "$OUT/ga_quality_sm.json" ;;
-    ls)    run bench_ls 600 python -u tools/bench_ls.py --pop 4096 --steps 200 ;;
-    ls1000) run bench_ls1000 600 python -u tools/bench_ls.py --pop 4096 --steps 1000 --cpu-sample 256 ;;
+    ls)    run bench_ls 300 python -u tools/bench_ls.py --pop 4096 --steps 200 --cpu-sample 256 ;;
+    ls1000) run bench_ls1000 300 python -u tools/bench_ls.py --pop 4096 --steps 1000 --pre-steps 3000 --cpu-sample 256 ;;
+    ga8k)  run ga8k 400 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 512 ;;
+    ga32k) run ga32k 300 python -u tools/bench_ga.py --config comp01 --pop 65536 --children 32768 --gens 10 --min-seconds 1.0 --steps 1000 --warm-gens 30 --warm-feasible 0.6 --cpu-sample 0 ;;
+    gatrace) run ga8k_trace 400 rocprofv3 --kernel-trace --stats -d "$OUT/ga_trace" -o run --output-format csv -- python -u tools/bench_ga.py $GA8K --gens 20 --cpu-sample 0 ;;
+    lsprof) run lsprof_ga 300 python -u tools/ls_prof.py --config comp01 --pop 65536 --children 8192 --from-ga 0.6 --steps 1000 ;;
+    timeprob) run time_problem 600 python -u tools/time_problem.py "$OUT/time_problem.json" 5 ;;
+    profderive) run rocprof_derive 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_derive" -o run --output-format csv -- python -u tools/time_problem.py "$OUT/time_problem_traced.json" 5 ;;
+    pmcderive) pmc pmc_derive derive_corr_kernel python -u tools/time_problem.py "$OUT/time_problem_pmc.json" 3 ;;
     listpmc) run listpmc 120 rocprofv3 -L ;;
-    pmc1)  run pmc1 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS --output-format csv -d "$OUT/pmc1" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
-    pmc2)  run pmc2 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc2" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
+    pmc1)  run pmc1 120 rocprofv3 --pmc $PASS1 --output-format csv -d "$OUT/pmc1" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
+    pmc2)  run pmc2 120 rocprofv3 --pmc $PASS2 --output-format csv -d "$OUT/pmc2" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
     pmc3)  run pmc3 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc3" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
     pmc4)  run pmc4 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc4" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
+    pmcls) pmc pmc_ls local_search_kernel python -u tools/bench_ls.py --cpu-sample 0 --reps 1 --pop 4096 --steps 1000 --pre-steps 3000 ;;
+    pmcga) pmc pmc_ga local_search_kernel python -u tools/bench_ga.py $GA8K --gens 10 --cpu-sample 0 ;;
+    pmcwide) pmc pmc_wide eval_ python -u tools/eval_variants.py syn 65536 13 ;;
+    abls)  run ab_comp01 400 python -u tools/ab_ls.py comp01 8192 old new && run ab_med 400 python -u tools/ab_ls.py med 4096 old new ;;
+    abeval) run ab_eval 300 python -u tools/ab_eval.py old new ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python -u bench.py --no-pmc --no-cpu --steps 100 ;;
+    *) echo "unknown step $s"; exit 2 ;;
   esac
 done
 echo "done"
