@@ -6,6 +6,10 @@ one independent population shard per rank, no data-path collective).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config med|lg|syn|sm]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+TTGA_BENCH_FORCE_DIST=1 initialises the process group (RCCL) at world 1 too, so
+the timing barrier and the MAX all-reduce run through RCCL on a one-GPU box
+(tests/test_gpu_bench.py); the numbers are the same workload.
+
 A step is one tt_eval over the rank's whole population. Rank 0 prints one JSON
 line (BASELINE.json metric) with the dominant kernel's roofline and, at N=1, a
 CPU baseline: the reference's own computeFeasibility/Hcv/Scv (oracle/_ref,
@@ -56,6 +60,13 @@ def parse():
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 counter passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def host_cores():
@@ -146,7 +157,13 @@ def main():
     # let a one-GPU box rehearse the N > 1 path (RCCL needs distinct GPUs)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     backend = os.environ.get("TTGA_BENCH_BACKEND", "nccl")
-    if world > 1:
+    use_dist = world > 1 or os.environ.get("TTGA_BENCH_FORCE_DIST", "") not in ("", "0")
+    if use_dist and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if use_dist:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -180,7 +197,7 @@ def main():
 
     stream = torch.cuda.current_stream(dev)      # tt_eval launches its one kernel on this stream
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -189,13 +206,13 @@ def main():
         dp.eval(slot, room, variant=args.variant, out=out)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
 
     t = torch.tensor([wall], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    if world > 1:
+    if use_dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
 
@@ -233,6 +250,40 @@ def main():
                                                                           "calib_bytes")}
             line["roofline"]["pipes"] = {k: pmc[k] for k in ("lds_busy", "lds_conflict", "valu_busy", "salu_busy",
                                                             "wait_any", "cycles") if k in pmc}
+            raw = pmc.get("raw", {})
+            if "SQ_LDS_IDX_ACTIVE" in raw and pmc.get("cycles"):
+                # the unit that binds these kernels is the LDS (and the issue around it), not HBM:
+                # LDS-array cycles per individual against one LDS cycle per CU per shader cycle
+                clk = pmc["cycles"] / (kernel_ms * 1e-3)
+                line["roofline"]["binding_unit"] = {
+                    "unit": "LDS-array cycles (SQ_LDS_IDX_ACTIVE, live pass)",
+                    "lds_cycles_per_individual": raw["SQ_LDS_IDX_ACTIVE"] / P,
+                    "peak": "1 LDS-array cycle per CU per shader cycle (MI355X_MICROARCH.md §LDS)",
+                    "frac": pmc.get("lds_busy"), "bank_conflict_share": pmc.get("lds_conflict"),
+                    "lds_only_us": raw["SQ_LDS_IDX_ACTIVE"] / (256 * clk) * 1e6,
+                    "valu_frac": pmc.get("valu_busy"), "salu_frac": pmc.get("salu_busy"),
+                    "clock_ghz": clk / 1e9}
+        if variant == 13 and not args.pmc_child:
+            # the wide path's lane phase alone (eval_lanes: variant bit 6 skips eval_corr), on
+            # the LDS byte-gather roofline: one ds_read_u8 per (individual, student id), 64 per
+            # wave-instruction in 2 LDS cycles (32 banks) = 32 lookups per CU per shader cycle
+            lookups = float(sum(n + (n & 1) for n in inst.student_events.sum(axis=1).tolist()))
+            ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ea.record(stream)
+            for _ in range(5):
+                dp.eval(slot, room, variant=13 | (4 << 4), out=out)
+            eb.record(stream)
+            torch.cuda.synchronize(dev)
+            lanes_ms = ea.elapsed_time(eb) / 5
+            dp.eval(slot, room, variant=args.variant, out=out)        # restore the full outputs
+            torch.cuda.synchronize(dev)
+            clk = pmc["cycles"] / (kernel_ms * 1e-3) if pmc and pmc.get("cycles") else 2.4e9
+            rate = P * lookups / (lanes_ms * 1e-3)
+            line["roofline"]["lane_phase"] = {
+                "kernel": "eval_lanes_w16", "kernel_ms": lanes_ms, "lookups_per_individual": lookups,
+                "lookups_per_s": rate, "peak_lookups_per_s": 32 * 256 * clk,
+                "frac": rate / (32 * 256 * clk), "clock_ghz": clk / 1e9,
+                "peak_note": "ds_read_u8: 64 lanes in 2 LDS cycles (32 banks) per CU; clock from the live pass"}
         if world == 1 and not args.no_cpu:
             n = args.cpu_sample
             if n <= 0:      # calibrate on a small slice, then size the sample to ~cpu_seconds
@@ -244,8 +295,10 @@ def main():
             s_np, r_np = slot[:n].cpu().numpy(), room[:n].cpu().numpy()
             gpu_out = [o[:n].cpu().numpy() for o in out]
             line["cpu_baseline"] = cpu_baseline(inst, s_np, r_np, gpu_out)
+        if use_dist and world == 1:
+            line["config"]["process_group"] = f"{backend} at world 1 (TTGA_BENCH_FORCE_DIST)"
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

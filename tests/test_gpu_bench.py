@@ -48,3 +48,15 @@ def test_bench_two_ranks_rehearsal():
     d = _line(r.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_pop"] == 2 * 65536 and d["value"] > 0
     assert "rehearsal" in d["config"] and "cpu_baseline" not in d
+
+
+def test_bench_rccl_process_group_one_gpu():
+    """TTGA_BENCH_FORCE_DIST=1: the nccl (RCCL) process group at world 1, so the
+    timing barrier and the MAX all-reduce of the N > 1 path run through RCCL
+    on a one-GPU box; the line is the N = 1 line."""
+    env = dict(os.environ, TTGA_BENCH_FORCE_DIST="1")
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "10", "--warmup", "2", "--no-pmc", "--no-cpu"],
+                       cwd=REPO, capture_output=True, text=True, timeout=280, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 1 and d["value"] > 0 and d["config"]["process_group"].startswith("nccl")

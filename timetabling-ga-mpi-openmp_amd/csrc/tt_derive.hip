@@ -3,18 +3,24 @@
 // students, studentNumber from the diagonal of the same product, and
 // possibleRooms from it in the diagonal tiles' epilogue.
 //
-//   A   [S][E] u8 0/1 (student_events, student-major as the .tim holds it)
-//   At  [Ep][Sp] u8   event-major copy, Ep = E rounded up to 64, Sp = S rounded
-//                     up to 64, zero padded (derive_transpose_kernel)
+//   Atb [Ep][Sp/32] u32  event-major BIT image of student_events: bit s of
+//                     event e's row is A[s][e]; Ep = E rounded up to 64, Sp = S
+//                     rounded up to 512, zero padded (derive_layout, built by the
+//                     host from the CSR it needs anyway: one pass over the
+//                     nonzeros). 1.3 MB at syn: the operands stay in L2.
 //   C = At · Atᵀ      C[i][j] = #students attending both i and j; C[i][i] =
 //                     studentNumber[i] since A is 0/1
 //
 // Mapping: one 4-wave workgroup per 64×64 block (bi <= bj) of C, one 32×32
 // quadrant per wave, v_mfma_i32_32x32x32_i8 over 32 students per step with
-// exact i32 accumulation. Both operands of a step are 16 consecutive students
-// of one event row per lane (a 16-B load): lane l holds row (l & 31) of its
-// operand tile at students 16·(l >> 5) .. +15, for A (events i) and for B
-// (events j) alike, so the k order is the same on both sides. C is symmetric,
+// exact i32 accumulation. Lane l holds row (l & 31) of its operand tile at
+// students 16·(l >> 5) .. +15 of the step: 16 bits of the row's step word,
+// expanded in registers to 16 bytes of 0/1 (per nibble x: x·0x00204081 &
+// 0x01010101 puts bit k in byte k), for A (events i) and B (events j) alike,
+// so the k order is the same on both sides. A lane loads 128 students (four
+// steps) of its row with one 16-B load, four such chunks ahead of the MFMAs
+// that use them (the loads are L2 hits; one chunk ahead left the wave waiting
+// on each: 37.5 us at syn). C is symmetric,
 // so an off-diagonal block's quadrant is written twice: its rows (ballots of
 // C > 0 per accumulator register) and its columns (the bits of a lane's own
 // accumulators, the two lane halves OR-ed). The image parts written:
@@ -33,28 +39,12 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-// A [S][E] -> At [Ep][Sp], 64×64 byte tiles through LDS, zero padded.
-__global__ __launch_bounds__(256) void derive_transpose_kernel(const uint8_t* __restrict__ A, int S, int E,
-                                                               uint8_t* __restrict__ At, int Sp) {
-    __shared__ uint8_t tile[64][65];
-    const int s0 = blockIdx.x * 64, e0 = blockIdx.y * 64, t = threadIdx.x;
-    for (int k = t; k < 64 * 64; k += 256) {
-        const int s = s0 + (k >> 6), e = e0 + (k & 63);
-        tile[k >> 6][k & 63] = (s < S && e < E) ? A[(size_t)s * E + e] : (uint8_t)0;
-    }
-    __syncthreads();
-    // thread t: event row e0 + (t >> 2), 16 students at 16·(t & 3)
-    const int r = t >> 2, q = (t & 3) * 16;
-    v4i w;
-    uint32_t* wp = (uint32_t*)&w;
+// 16 bits (students k..k+15 of a row) -> 16 bytes of 0/1, byte j = bit j
+__device__ __forceinline__ v4i bits_to_bytes(uint32_t h16) {
+    v4i v;
 #pragma unroll
-    for (int d = 0; d < 4; d++) {
-        uint32_t x = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) x |= (uint32_t)tile[q + 4 * d + b][r] << (8 * b);
-        wp[d] = x;
-    }
-    *(v4i*)(At + (size_t)(e0 + r) * Sp + s0 + q) = w;
+    for (int d = 0; d < 4; d++) v[d] = (int)((__builtin_amdgcn_ubfe(h16, 4 * d, 4) * 0x00204081u) & 0x01010101u);
+    return v;
 }
 
 struct DeriveOut {
@@ -81,7 +71,7 @@ __device__ __forceinline__ void put_row_word(const DeriveOut& o, int E, int EW, 
     o.cupT[((size_t)(j0 >> 6) * E + i) * 2 + (wd & 1)] = up;
 }
 
-__global__ __launch_bounds__(256) void derive_corr_kernel(const uint8_t* __restrict__ At, int E, int Sp, int nb,
+__global__ __launch_bounds__(256) void derive_corr_kernel(const uint32_t* __restrict__ Atb, int E, int Sp, int nb,
                                                           const int32_t* __restrict__ room_size, int R,
                                                           const uint64_t* __restrict__ efw,
                                                           const uint64_t* __restrict__ rfw, int FW, DeriveOut o) {
@@ -96,23 +86,28 @@ __global__ __launch_bounds__(256) void derive_corr_kernel(const uint8_t* __restr
     const int i0 = 64 * bi + 32 * qi, j0 = 64 * bj + 32 * qj;
     const int r = lane & 31, h = lane >> 5;
 
-    const uint8_t* pa = At + (size_t)(i0 + r) * Sp + 16 * h;
-    const uint8_t* pb = At + (size_t)(j0 + r) * Sp + 16 * h;
+    const int SW = Sp >> 5, nch = SW >> 2;                     // u32 words per bit row, 128-student chunks
+    const v4i* pa = (const v4i*)(Atb + (size_t)(i0 + r) * SW);
+    const v4i* pb = (const v4i*)(Atb + (size_t)(j0 + r) * SW);
+    const int sh = 16 * h;
     v16i acc = {};
-    int s = 0;
-    for (; s + 128 <= Sp; s += 128) {                          // four steps, eight loads in flight
-        v4i a0 = *(const v4i*)(pa + s), b0 = *(const v4i*)(pb + s);
-        v4i a1 = *(const v4i*)(pa + s + 32), b1 = *(const v4i*)(pb + s + 32);
-        v4i a2 = *(const v4i*)(pa + s + 64), b2 = *(const v4i*)(pb + s + 64);
-        v4i a3 = *(const v4i*)(pa + s + 96), b3 = *(const v4i*)(pb + s + 96);
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a2, b2, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a3, b3, acc, 0, 0, 0);
+    constexpr int PD = 4;                                      // chunks in flight (nch is a multiple of PD)
+    v4i ra[PD], rb[PD];
+#pragma unroll
+    for (int k = 0; k < PD; k++) {
+        ra[k] = k < nch ? pa[k] : v4i{};
+        rb[k] = k < nch ? pb[k] : v4i{};
     }
-    for (; s < Sp; s += 32) {
-        v4i a0 = *(const v4i*)(pa + s), b0 = *(const v4i*)(pb + s);
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc, 0, 0, 0);
+    for (int c = 0; c < nch; c += PD) {
+#pragma unroll
+        for (int k = 0; k < PD; k++) {
+            const v4i wa = ra[k], wb = rb[k];
+            if (c + PD + k < nch) { ra[k] = pa[c + PD + k]; rb[k] = pb[c + PD + k]; }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(bits_to_bytes((uint32_t)wa[q] >> sh),
+                                                            bits_to_bytes((uint32_t)wb[q] >> sh), acc, 0, 0, 0);
+        }
     }
 
     const int EW = (E + 31) >> 5, EW64 = (E + 63) >> 6;
@@ -161,37 +156,34 @@ __global__ __launch_bounds__(256) void derive_corr_kernel(const uint8_t* __restr
 
 }  // namespace
 
-int derive_on_device(const tt_problem* p, const uint8_t* A_host, const int32_t* room_size, const uint64_t* efw,
+int derive_on_device(const tt_problem* p, const uint32_t* atb, const int32_t* room_size, const uint64_t* efw,
                      const uint64_t* rfw, int FW) {
     const int E = p->E, S = p->S, R = p->R;
-    const int Ep = (E + 63) & ~63, Sp = (S + 63) & ~63, nb = Ep / 64;
-    const size_t a_bytes = ((size_t)S * E + 255) & ~(size_t)255, at_bytes = ((size_t)Ep * Sp + 255) & ~(size_t)255;
+    const DeriveLayout DL = derive_layout(E, S);
+    const int nb = DL.Ep / 64;
+    const size_t at_bytes = ((size_t)DL.Ep * DL.SW * 4 + 255) & ~(size_t)255;
     const size_t rs_bytes = 256 * ((sizeof(int32_t) * R + 255) / 256);
     const size_t ef_bytes = ((sizeof(uint64_t) * E * FW) + 255) & ~(size_t)255;
     const size_t rf_bytes = ((sizeof(uint64_t) * R * FW) + 255) & ~(size_t)255;
-    const size_t total = a_bytes + at_bytes + rs_bytes + ef_bytes + rf_bytes + 256;
+    const size_t total = at_bytes + rs_bytes + ef_bytes + rf_bytes + 256;
     uint8_t* tmp = nullptr;
     hipStream_t st = nullptr;
     TT_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     hipError_t he = hipMalloc(&tmp, total);
     if (he != hipSuccess) { (void)hipStreamDestroy(st); return check_hip(he, "derive: hipMalloc"); }
-    uint8_t* dA = tmp;
-    uint8_t* dAt = dA + a_bytes;
-    int32_t* drs = (int32_t*)(dAt + at_bytes);
+    uint32_t* dAt = (uint32_t*)tmp;
+    int32_t* drs = (int32_t*)(tmp + at_bytes);
     uint64_t* def = (uint64_t*)((uint8_t*)drs + rs_bytes);
     uint64_t* drf = (uint64_t*)((uint8_t*)def + ef_bytes);
     const DevProblem& d = p->dev;
     DeriveOut o{const_cast<uint32_t*>(d.corr), (uint32_t*)const_cast<uint64_t*>(d.corr64),
                 (uint32_t*)const_cast<uint64_t*>(d.cupT), const_cast<int32_t*>(d.sn), const_cast<uint64_t*>(d.poss)};
-    if (S > 0) he = hipMemcpyAsync(dA, A_host, (size_t)S * E, hipMemcpyHostToDevice, st);
+    if (DL.SW > 0) he = hipMemcpyAsync(dAt, atb, (size_t)DL.Ep * DL.SW * 4, hipMemcpyHostToDevice, st);
     if (he == hipSuccess) he = hipMemcpyAsync(drs, room_size, sizeof(int32_t) * R, hipMemcpyHostToDevice, st);
     if (he == hipSuccess && FW > 0) he = hipMemcpyAsync(def, efw, sizeof(uint64_t) * E * FW, hipMemcpyHostToDevice, st);
     if (he == hipSuccess && FW > 0) he = hipMemcpyAsync(drf, rfw, sizeof(uint64_t) * R * FW, hipMemcpyHostToDevice, st);
-    if (he == hipSuccess && Sp > 0)
-        hipLaunchKernelGGL(derive_transpose_kernel, dim3(Sp / 64, Ep / 64), dim3(256), 0, st, dA, S, E, dAt, Sp);
-    if (he == hipSuccess) he = hipGetLastError();
     if (he == hipSuccess)
-        hipLaunchKernelGGL(derive_corr_kernel, dim3(nb * (nb + 1) / 2), dim3(256), 0, st, dAt, E, Sp, nb, drs, R, def,
+        hipLaunchKernelGGL(derive_corr_kernel, dim3(nb * (nb + 1) / 2), dim3(256), 0, st, dAt, E, DL.Sp, nb, drs, R, def,
                            drf, FW, o);
     if (he == hipSuccess) he = hipGetLastError();
     if (he == hipSuccess) he = hipStreamSynchronize(st);

@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <type_traits>
 #include <utility>
+#include <vector>
 
 #include "tt_internal.h"
 
@@ -212,8 +213,46 @@ __device__ __forceinline__ int mask_scv(uint64_t m) {
     for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);
     return sc;
 }
+// The same terms for a mask in the GAPPED slot layout of eval_lanes' tile
+// (TT_LANES_GAP): slot s = 9d + k sits at bit 10d + k for days 0-2 and at bit
+// 32 + 10(d - 3) + k for days 3-4, so every day is a 9-bit field followed by a
+// zero bit and no field straddles the 32-bit halves (the tile's sentinel
+// column keeps bit 63). Then:
+//  * >2 in a row: m & m>>1 & m>>2 cannot cross a day (the zero bit), no mask;
+//  * single class, per half, every field f at once: b = x + K (K = 511 per
+//    field, no carry out of a field) has the field's top bit set iff f != 0 and
+//    its low bits f - 1, so t = x & b is f & (f - 1) per field, and
+//    [popcount(f) == 1] = top bit of b and not of t + K. 14 VALU for the five
+//    days instead of 21 (bfe, bcnt, compare, add per day).
+constexpr uint32_t kGapLoK = 0x1FF7FDFFu, kGapLoG = 0x20080200u;    // fields at bits 0, 10, 20
+constexpr uint32_t kGapHiK = 0x0007FDFFu, kGapHiG = 0x00080200u;    // fields at bits 32, 42
+__device__ __forceinline__ int mask_scv_gap(uint64_t m) {
+    int sc = __popcll(m & (m >> 1) & (m >> 2));
+    const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+    const uint32_t blo = lo + kGapLoK, bhi = hi + kGapHiK;
+    const uint32_t tlo = (lo & blo) + kGapLoK, thi = (hi & bhi) + kGapHiK;
+    sc += __popc((blo ^ tlo) & kGapLoG);
+    sc += __popc((bhi ^ thi) & kGapHiG);
+    return sc;
+}
+// slot bytes -> gapped bit positions, four bytes of one row at a time (valid
+// slots < 45; a byte >= 128 of an invalid genome may spill into its row
+// neighbour, whose individual evaluates to the invalid sentinel anyway):
+// p = s + [s >= 9] + [s >= 18] + 3 [s >= 27] + [s >= 36]
+__device__ __forceinline__ uint32_t gap_slots4(uint32_t x) {
+    const uint32_t o = x | 0x80808080u;
+    const uint32_t g9 = ((o - 0x09090909u) >> 7) & 0x01010101u, g18 = ((o - 0x12121212u) >> 7) & 0x01010101u;
+    const uint32_t g27 = ((o - 0x1B1B1B1Bu) >> 7) & 0x01010101u, g36 = ((o - 0x24242424u) >> 7) & 0x01010101u;
+    return x + g9 + g18 + g36 + 3u * g27;
+}
+__device__ __forceinline__ uint8_t gap_slot(uint32_t s) { return (uint8_t)gap_slots4(s); }
+#ifndef TT_LANES_GAP
+#define TT_LANES_GAP 0
+#endif
+template <bool GAP>
+__device__ __forceinline__ int mask_terms(uint64_t m) { return GAP ? mask_scv_gap(m) : mask_scv(m); }
 // K students of N ids whose dwords are r[0 .. K*N/2)
-template <int N, int K>
+template <int N, int K, bool GAP = false>
 __device__ __forceinline__ int students_scv(const uint8_t* my, const u32x16& r) {
     constexpr int H = N / 2;
     uint32_t sl[K * N];
@@ -227,14 +266,14 @@ __device__ __forceinline__ int students_scv(const uint8_t* my, const u32x16& r) 
         uint64_t m = 0;
 #pragma unroll
         for (int j = 0; j < N; ++j) m |= 1ull << (sl[k * N + j] & 63);
-        sc += mask_scv(m);
+        sc += mask_terms<GAP>(m);
     }
     return sc;
 }
 // A run of cnt students of N ids from dword p: one 64-B scalar load per step
 // (two students when N <= 16), the next step's load issued before this step's
 // LDS reads (ping-pong registers).
-template <int N, int KMAX>
+template <int N, int KMAX, bool GAP = false>
 __device__ __forceinline__ int run_scv(const uint8_t* my, const uint32_t* p, int cnt) {
     constexpr int K = N <= 16 ? KMAX : 1;
     constexpr int ST = K * N / 2;
@@ -258,7 +297,7 @@ __device__ __forceinline__ int run_scv(const uint8_t* my, const uint32_t* p, int
             uint64_t m = 0;
 #pragma unroll
             for (int j = 0; j < N; ++j) m |= 1ull << (sl[j] & 63);
-            sc += mask_scv(m);
+            sc += mask_terms<GAP>(m);
 #pragma unroll
             for (int j = 0; j < N / 2; ++j) cur[j] = nxt[j];
         }
@@ -270,11 +309,11 @@ __device__ __forceinline__ int run_scv(const uint8_t* my, const uint32_t* p, int
         while (true) {
             sld_wait(ra);
             rb = sload16(p + (i + 1 < steps ? i + 1 : i) * ST);
-            sc += students_scv<N, K>(my, ra);
+            sc += students_scv<N, K, GAP>(my, ra);
             if (++i == steps) { sld_wait(rb); break; }
             sld_wait(rb);
             ra = sload16(p + (i + 1 < steps ? i + 1 : i) * ST);
-            sc += students_scv<N, K>(my, rb);
+            sc += students_scv<N, K, GAP>(my, rb);
             if (++i == steps) { sld_wait(ra); break; }
         }
     }
@@ -282,13 +321,13 @@ __device__ __forceinline__ int run_scv(const uint8_t* my, const uint32_t* p, int
         if (cnt & 1) {
             u32x16 r = sload16(p + steps * ST);
             sld_wait(r);
-            sc += students_scv<N, 1>(my, r);
+            sc += students_scv<N, 1, GAP>(my, r);
         }
     }
     return sc;
 }
 // students of more than 32 ids (no instance here has them): plain loop
-__device__ __noinline__ int run_scv_any(const uint8_t* my, const ConstU32* p, int cnt, int n) {
+__device__ __noinline__ int run_scv_any(const uint8_t* my, const ConstU32* p, int cnt, int n, bool gap) {
     int sc = 0;
     for (int i = 0; i < cnt; ++i) {
         uint64_t m = 0;
@@ -297,11 +336,11 @@ __device__ __noinline__ int run_scv_any(const uint8_t* my, const ConstU32* p, in
             m |= 1ull << (my[d & 0xFFFFu] & 63);
             m |= 1ull << (my[d >> 16] & 63);
         }
-        sc += mask_scv(m);
+        sc += gap ? mask_scv_gap(m) : mask_scv(m);
     }
     return sc;
 }
-template <int KMAX>
+template <int KMAX, bool GAP = false>
 __device__ __forceinline__ int lane_scv_runs(const uint8_t* my, const DevProblem& pb, int r0, int r1) {
     const ConstI32* runs = (const ConstI32*)pb.srun;
     int sc = 0;
@@ -309,11 +348,11 @@ __device__ __forceinline__ int lane_scv_runs(const uint8_t* my, const DevProblem
         const int n = runs[4 * k], off = runs[4 * k + 1], cnt = runs[4 * k + 2];
         const uint32_t* p = pb.sid + off;
         switch (n) {
-#define TT_RUN(N) case N: sc += run_scv<N, KMAX>(my, p, cnt); break;
+#define TT_RUN(N) case N: sc += run_scv<N, KMAX, GAP>(my, p, cnt); break;
             TT_RUN(2) TT_RUN(4) TT_RUN(6) TT_RUN(8) TT_RUN(10) TT_RUN(12) TT_RUN(14) TT_RUN(16)
             TT_RUN(18) TT_RUN(20) TT_RUN(22) TT_RUN(24) TT_RUN(26) TT_RUN(28) TT_RUN(30) TT_RUN(32)
 #undef TT_RUN
-            default: sc += run_scv_any(my, (const ConstU32*)p, cnt, n); break;
+            default: sc += run_scv_any(my, (const ConstU32*)p, cnt, n, GAP); break;
         }
     }
     return sc;
@@ -395,6 +434,16 @@ __device__ __forceinline__ void tile_dma(const uint8_t* src, uint8_t* dst, int n
 #endif
 }
 
+// Profiling build (-DTT_T5_STAMP, libttga_prof.so, tools/t5_stamps.py): per
+// workgroup, the constant-clock time (s_memrealtime, 100 MHz) when its wave 0
+// starts and when each of its waves ends, and the hardware slot it ran on
+// (HW_ID, XCC_ID), for launch index (variant bits 12..14) of kT5Launches. No
+// atomics and no extra barrier: the stamps cost a few stores per wave.
+#ifdef TT_T5_STAMP
+constexpr int kT5Launches = 8, kT5MaxBlocks = 16384, kT5Words = 10;   // t0, id, end of waves 0..7
+__device__ unsigned long long g_t5_stamp[kT5Launches * kT5MaxBlocks * kT5Words];
+#endif
+
 template <int EWC, int NW, int PK, bool DB = false>
 __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
                                                               const uint8_t* __restrict__ room, int P,
@@ -405,6 +454,18 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int ablate = TT_EVAL_ABLATE ? ablate_arg : (ablate_arg & 3);   // phase skips: once per tile / batch
     constexpr int NT = 64 * NW;
+#ifdef TT_T5_STAMP
+    unsigned long long* st_rec =
+        g_t5_stamp + ((size_t)((ablate_arg >> 8) & (kT5Launches - 1)) * kT5MaxBlocks + (blockIdx.x % kT5MaxBlocks)) * kT5Words;
+    if (threadIdx.x == 0) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        st_rec[0] = t0;
+        st_rec[1] = ((unsigned long long)xcc << 32) | hw;
+    }
+#endif
     const int E = pb.E, R = pb.R;
     const int lane = threadIdx.x & 63, wv = wave_id();
     const Tile5Layout L = tile5_layout(E, R, NW, DB);
@@ -606,6 +667,9 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
             }
         }
     }
+#ifdef TT_T5_STAMP
+    if ((threadIdx.x & 63) == 0) st_rec[2 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // ---------------------------------------------------------------- eval_lanes
@@ -645,17 +709,24 @@ __global__ __launch_bounds__(64 * NWL) void eval_lanes_kernel(DevProblem pb, con
                 const int r = (int)(((uint64_t)(uint32_t)w * qinv) >> 32), c = w - r * qpr;
                 const uint4 v = s16[w];
                 uint32_t* d = (uint32_t*)(tile + r * SP + 16 * c);
-                d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+                if (TT_LANES_GAP) {
+                    d[0] = gap_slots4(v.x); d[1] = gap_slots4(v.y); d[2] = gap_slots4(v.z); d[3] = gap_slots4(v.w);
+                } else {
+                    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+                }
             }
         } else {
 #pragma unroll 1
             for (int r = wv; r < np; r += NWL)
 #pragma unroll 1
-                for (int c = lane; c < E; c += 64) tile[r * SP + c] = src[(long)r * E + c];
+                for (int c = lane; c < E; c += 64) {
+                    const uint8_t v = src[(long)r * E + c];
+                    tile[r * SP + c] = TT_LANES_GAP ? gap_slot(v) : v;
+                }
         }
         if (threadIdx.x < 64) tile[threadIdx.x * SP + E] = 63;
         __syncthreads();
-        const int sc = r0 < r1 ? lane_scv_runs<2>(tile + lane * SP, pb, r0, r1) : 0;
+        const int sc = r0 < r1 ? lane_scv_runs<2, TT_LANES_GAP != 0>(tile + lane * SP, pb, r0, r1) : 0;
         part[wv * 64 + lane] = sc;
         __syncthreads();
         if (wv == 0 && lane < np) {
@@ -1100,6 +1171,20 @@ static int auto_variant(const tt_problem* p) {
 }
 
 extern "C" int tt_eval_auto_variant(const tt_problem* p) { return p ? auto_variant(p) : -1; }
+
+#ifdef TT_T5_STAMP
+// profiling build: copies the stamp buffer ([launch][block][10] u64: wave 0's
+// start, XCC_ID << 32 | HW_ID, the end of waves 0..7) and, with reset, clears it
+extern "C" int tt_t5_stamp_read(unsigned long long* out, int reset) {
+    TT_HIP(hipDeviceSynchronize());
+    TT_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t5_stamp), sizeof(g_t5_stamp)));
+    if (reset) {
+        std::vector<unsigned long long> z(sizeof(g_t5_stamp) / 8, 0ull);
+        TT_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_t5_stamp), z.data(), sizeof(g_t5_stamp)));
+    }
+    return kT5Launches * kT5MaxBlocks;
+}
+#endif
 
 extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const uint8_t* room, int P, int32_t* hcv,
                                int32_t* scv, uint8_t* feasible, int32_t* penalty, int variant, void* stream) {

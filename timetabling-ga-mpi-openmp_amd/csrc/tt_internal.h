@@ -55,10 +55,24 @@ int check_pop_args(const tt_problem* p, int P, const void* a, const void* b);
 // Makes the handle's device current for the calling thread.
 int use_device(const tt_problem* p);
 
+// Bit image of the attendance matrix for the device derivation: Ep = E rounded
+// up to 64 event rows of SW u32 words, Sp = S rounded up to 512 students (four
+// 128-student chunks per prefetch group).
+struct DeriveLayout {
+    int Ep, Sp, SW;
+};
+inline DeriveLayout derive_layout(int E, int S) {
+    DeriveLayout L;
+    L.Ep = (E + 63) & ~63;
+    L.Sp = (S + 511) & ~511;
+    L.SW = L.Sp / 32;
+    return L;
+}
+
 // studentNumber, eventCorrelations (corr, corr64, cupT) and possibleRooms of
-// the image, derived on the handle's (current) device from the u8 attendance
-// matrix A[S][E] (csrc/tt_derive.hip); synchronous.
-int derive_on_device(const tt_problem* p, const uint8_t* A, const int32_t* room_size, const uint64_t* efw,
+// the image, derived on the handle's (current) device from the attendance bit
+// rows atb[Ep][SW] (derive_layout; csrc/tt_derive.hip); synchronous.
+int derive_on_device(const tt_problem* p, const uint32_t* atb, const int32_t* room_size, const uint64_t* efw,
                      const uint64_t* rfw, int FW);
 
 }  // namespace ttga

@@ -915,6 +915,8 @@ __device__ __forceinline__ uint64_t bperm64(uint64_t v, int src_lane) {
     return ((uint64_t)(uint32_t)bperm((int)(uint32_t)(v >> 32), src_lane) << 32) | (uint32_t)bperm((int)(uint32_t)v, src_lane);
 }
 
+__device__ __forceinline__ bool hot_bit(uint64_t hot, int e) { return (bperm64(hot, e >> 6) >> (e & 63)) & 1ull; }
+
 // Resolves a window of `rem` remaining trials (lanes k < rem) whose per-lane
 // full-path flag is `need`: returns the lane of the first trial to run in
 // full (64: none), with st/step advanced past it (its draw and step taken);
@@ -941,6 +943,39 @@ __device__ __forceinline__ int window_resolve(int lane, uint32_t jump, int64_t& 
     return kstar;
 }
 
+// TT_LS_HOT (phase 1): the events with eventHcv > 0 as a bitmask over event
+// ids, one 64-bit word per lane (lane w: events 64w..64w+63). A visit of an
+// event with eventHcv == 0 only counts towards evCount (no draw, no step:
+// Solution.cpp:509-512), so the visit loop jumps over such events 64 scramble
+// positions at a time instead of loading each one's correlation row. The flags
+// change only for the events of the slots an accepted move touches
+// (eventHcv(e) depends on e's slot only), which refresh_hot recomputes.
+#ifndef TT_LS_HOT
+#define TT_LS_HOT 0
+#endif
+// eventHcv(e) > 0 for events e = 64k + lane; with `all` every event, else only
+// those in a touched slot (S.ts, after accept) replace their flag in `hot`
+__device__ __forceinline__ uint64_t refresh_hot(const LsState& S, uint64_t hot, bool all) {
+    const int E = S.E, R = S.R, EW = S.EW, lane = S.lane;
+    for (int k = 0; 64 * k < E; ++k) {                        // wave-uniform
+        const int e = 64 * k + lane;
+        bool upd = false, h = false;
+        if (e < E) {
+            const int t = S.sl[e];
+            upd = all || (S.nts > 0 && t == S.ts[0]) || (S.nts > 1 && t == S.ts[1]) || (S.nts > 2 && t == S.ts[2]);
+            if (upd) {
+                int c = (int)S.hist[t * R + S.rr[e]] - 1;
+                const uint64_t* row = S.pb.corr64 + (size_t)e * EW;
+                for (int w = 0; w < EW; ++w) c += __popcll(row[w] & S.B[(size_t)t * EW + w]);
+                c -= (int)((row[e >> 6] >> (e & 63)) & 1ull);
+                h = c > 0;
+            }
+        }
+        const uint64_t um = ballot(upd), hm = ballot(h);
+        if (um && lane == k) hot = (hot & ~um) | hm;
+    }
+    return hot;
+}
 // One individual's localSearch by the calling wave (every lane). CAP =
 // matcher task capacity. redo_list (first launch, CAP = kLsCapSmall): an
 // individual that overflowed a task is appended to it (redo_list[0] counts,
@@ -1084,18 +1119,43 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
         // TT_LS_ROWPF: the visited event's correlation row loaded one visit ahead
         // (the scrambled event list is fixed, so the next visit's event is known)
         uint64_t nrow = (fast1 && TT_LS_ROWPF) ? load_row(S, S.evl[0]) : 0ull;
+        const bool hotm = TT_LS_HOT && fast1;
+        uint64_t hot = hotm ? refresh_hot(S, 0ull, true) : 0ull;
         for (int i = 0; evc < E; i = (i + 1) % E) {
             if (step > max_steps || ++guard > guard_max) break;
+            if (hotm) {
+                // jump to the next event with eventHcv > 0 (each one skipped is a visit
+                // that only counts towards evCount); the loop ends after E in a row
+                bool out = false;
+                for (;;) {
+                    const int rem = E - evc;                            // visits left before the loop ends
+                    int pk = i + lane;
+                    while (pk >= E) pk -= E;
+                    const uint64_t hb = ballot(hot_bit(hot, S.evl[pk]) && lane < rem);
+                    if (hb) {
+                        const int k = __builtin_ctzll(hb);
+                        evc += k; guard += k;
+                        i = (i + k) % E;
+                        break;
+                    }
+                    const int n = rem < 64 ? rem : 64;
+                    evc += n; guard += n;
+                    i = (i + n) % E;
+                    if (evc >= E) { out = true; break; }
+                }
+                if (out || guard > guard_max) break;
+            }
             const int ei = S.evl[i];
             LSP_CNT(S, kPfVisits);
             LSP_T(t_vis);
             uint64_t row = nrow;
             if (fast1 && TT_LS_ROWPF) nrow = load_row(S, S.evl[i + 1 < E ? i + 1 : 0]);
             else if (fast1) row = load_row(S, ei);
-            // eventHcv(ei) (Solution.cpp:173-191)
-            const int ehcv = fast1 ? (int)S.hist[S.sl[ei] * R + S.rr[ei]] - 1 +
-                                         row_in_set(S, row, S.B + (size_t)S.sl[ei] * EW) - (int)row_bit(row, ei)
-                                   : ehcv_cur(S, ei);
+            // eventHcv(ei) (Solution.cpp:173-191); known > 0 from the flags
+            const int ehcv = hotm ? 1
+                             : fast1 ? (int)S.hist[S.sl[ei] * R + S.rr[ei]] - 1 +
+                                           row_in_set(S, row, S.B + (size_t)S.sl[ei] * EW) - (int)row_bit(row, ei)
+                                     : ehcv_cur(S, ei);
             if (ehcv == 0) { evc++; LSP_ADD(S, kPfVis1, t_vis); continue; }
             const int t_orig = S.sl[ei];
             Visit2 V;
@@ -1146,11 +1206,11 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         if (lb >= c) { S.c1_valid = 1; continue; }
                         LSP_CNT(S, kPfP1m1m);
                         if (match_tasks(S, 1)) goto redo;
-                        if (lb + S.misc[0] < c) { LSP_CNT(S, kPfP1m1a); accept(S); evc = 0; better = true; break; }
+                        if (lb + S.misc[0] < c) { LSP_CNT(S, kPfP1m1a); accept(S); if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
                     } else {
                         if (match_tasks(S, 7)) goto redo;
                         const int n = eah_nb(S, ei) + S.misc[task_of(S, t_orig)];
-                        if (n < c) { accept(S); evc = 0; better = true; break; }
+                        if (n < c) { accept(S); if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
                     }
                     reject_move1(S);
                 }
@@ -1227,7 +1287,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                             if (match_tasks(S, 2, tr)) goto redo;
                         } else if (match_tasks(S, 7, tr)) goto redo;
                         const int n = lb + S.misc[task_of(S, slot_nb(S, ei))] + S.misc[task_of(S, slot_nb(S, ej))];
-                        if (n < c) { accept(S); acc = true; break; }
+                        if (n < c) { accept(S); if (hotm) hot = refresh_hot(S, hot, false); acc = true; break; }
                         sync_rooms(S, false);
                     } while (0);
                     if (acc) { evc = 0; better = true; break; }
@@ -1248,7 +1308,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                             set_move(S, 3, ei, ej, ek);
                             if (build_and_match(S)) goto redo;
                             const int n = eah_nb(S, ei) + eah_nb(S, ej) + eah_nb(S, ek);
-                            if (n < c) { accept(S); evc = 0; better = true; break; }
+                            if (n < c) { accept(S); if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
                             sync_rooms(S, false);
                         }
                         if (step > max_steps) break;
@@ -1258,7 +1318,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                             set_move(S, 3, ei, ek, ej);
                             if (build_and_match(S)) goto redo;
                             const int n = eah_nb(S, ei) + eah_nb(S, ek) + eah_nb(S, ej);
-                            if (n < c) { accept(S); evc = 0; better = true; break; }
+                            if (n < c) { accept(S); if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
                             sync_rooms(S, false);
                         }
                     }

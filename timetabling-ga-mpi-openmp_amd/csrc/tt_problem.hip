@@ -59,23 +59,27 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     for (long i = 0; i < (long)E * F; i++)
         if (event_feat[i] != 0 && event_feat[i] != 1) { set_error("event_features must be 0/1"); return TT_ERR_INVALID; }
 
-    // One pass over student_events: the 0/1 check, the u8 copy the device
-    // derivation uploads, and the two CSR views (the students' events and the
-    // events' students) that the kernels read. The event degrees of the CSR are
-    // studentNumber; the device derives it again from the diagonal of AᵀA and
-    // the two must agree (checked below).
-    std::vector<uint8_t> a8((size_t)S * E);
+    // One pass over student_events: the 0/1 check and the two CSR views (the
+    // students' events and the events' students) that the kernels read. The
+    // event degrees of the CSR are studentNumber; the device derives it again
+    // from the diagonal of AᵀA and the two must agree (checked below).
     std::vector<int32_t> stu_off(S + 1, 0), stu_ev, ev_off(E + 1, 0), ev_stu, degree(E, 0);
     for (int s = 0; s < S; s++) {
         const int32_t* row = A + (size_t)s * E;
-        uint8_t* out8 = a8.data() + (size_t)s * E;
         int32_t bad = 0;
-        for (int e = 0; e < E; e++) { bad |= row[e] & ~1; out8[e] = (uint8_t)row[e]; }
+        for (int e = 0; e < E; e++) bad |= row[e] & ~1;
         if (bad) { set_error("student_events must be 0/1"); return TT_ERR_INVALID; }
         for (int e = 0; e < E; e++)
-            if (out8[e]) { stu_ev.push_back(e); degree[e]++; }
+            if (row[e]) { stu_ev.push_back(e); degree[e]++; }
         stu_off[s + 1] = (int32_t)stu_ev.size();
     }
+    // the attendance matrix as event-major bit rows for the device's AᵀA
+    // (csrc/tt_derive.hip derive_layout): bit s of row e = A[s][e], one pass
+    // over the nonzeros (1.3 MB at syn instead of a 10-40 MB upload)
+    const DeriveLayout DL = derive_layout(E, S);
+    std::vector<uint32_t> atb((size_t)DL.Ep * DL.SW, 0u);
+    for (int s = 0; s < S; s++)
+        for (int k = stu_off[s]; k < stu_off[s + 1]; k++) atb[(size_t)stu_ev[k] * DL.SW + (s >> 5)] |= 1u << (s & 31);
 
     tt_problem* p = new tt_problem();
     p->E = E; p->R = R; p->F = F; p->S = S; p->device = device;
@@ -215,7 +219,7 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     int rc = TT_OK;
     he = hipSetDevice(device);
     if (he != hipSuccess) rc = check_hip(he, "tt_problem_create");
-    if (rc == TT_OK) rc = derive_on_device(p, a8.data(), room_size, efw.data(), rfw.data(), FW);
+    if (rc == TT_OK) rc = derive_on_device(p, atb.data(), room_size, efw.data(), rfw.data(), FW);
     // host copies for tt_problem_derived and the kernels' launch choices
     p->student_number.assign(E, 0);
     p->poss_bits.assign(E, 0ull);

@@ -5,7 +5,7 @@
 # usage: tools/gpu_check.sh [tag] [steps...]
 #   tests gatests derive smoke bench prof benchsyn profsyn benchlg phases quality
 #   ls ls1000 ga8k ga32k gatrace lsprof timeprob profderive pmcderive listpmc
-#   pmc1..pmc4 (headline eval) pmcls (phase-2 local search) pmcga (GA children's
+#   stamps replace ablanes pmc1..pmc4 (headline eval) pmcls (phase-2 local search) pmcga (GA children's
 #   local search) pmcwide (syn wide path) abls abeval
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -62,7 +62,12 @@ for s in $STEPS; do
     lsprof) run lsprof_ga 300 python -u tools/ls_prof.py --config comp01 --pop 65536 --children 8192 --from-ga 0.6 --steps 1000 ;;
     timeprob) run time_problem 600 python -u tools/time_problem.py "$OUT/time_problem.json" 5 ;;
     profderive) run rocprof_derive 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_derive" -o run --output-format csv -- python -u tools/time_problem.py "$OUT/time_problem_traced.json" 5 ;;
-    pmcderive) pmc pmc_derive derive_corr_kernel python -u tools/time_problem.py "$OUT/time_problem_pmc.json" 3 ;;
+    pmcderive)
+        for c in "SQ_INSTS_VALU_MFMA_I8 SQ_INSTS_VALU_MFMA_MOPS_I8 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA SQ_WAIT_ANY GRBM_GUI_ACTIVE" "FETCH_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAVES SQ_INSTS_LDS"; do
+            i=$(( ${i:-0} + 1 ))
+            run pmc_derive$i 150 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_derive/p$i" -o pmc -- python -u tools/time_problem.py "$OUT/time_problem_pmc$i.json" 3 syn
+        done
+        python tools/pmc_summary.py "$OUT/pmc_derive" derive_corr_kernel > "$OUT/pmc_derive.json"; cat "$OUT/pmc_derive.json" ;;
     listpmc) run listpmc 120 rocprofv3 -L ;;
     pmc1)  run pmc1 120 rocprofv3 --pmc $PASS1 --output-format csv -d "$OUT/pmc1" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
     pmc2)  run pmc2 120 rocprofv3 --pmc $PASS2 --output-format csv -d "$OUT/pmc2" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
@@ -72,6 +77,11 @@ for s in $STEPS; do
     pmcga) pmc pmc_ga local_search_kernel python -u tools/bench_ga.py $GA8K --gens 10 --cpu-sample 0 ;;
     pmcwide) pmc pmc_wide eval_ python -u tools/eval_variants.py syn 65536 13 ;;
     abls)  run ab_comp01 400 python -u tools/ab_ls.py comp01 8192 old new && run ab_med 400 python -u tools/ab_ls.py med 4096 old new ;;
+    stamps) run t5_stamps 300 python -u tools/t5_stamps.py ;;
+    replace) run time_replace 300 python -u tools/time_replace.py ;;
+    ablanes) run ab_lanes 400 python -u tools/ab_eval.py syn 262144 gap0:13 gap1:13 gap0:77 gap1:77 ;;
+    abhot) run ab_hot_comp01 400 python -u tools/ab_ls.py comp01 8192 hot0 hot1 && run ab_hot_med 400 python -u tools/ab_ls.py med 4096 hot0 hot1 ;;
+    gahot) for i in 1 2; do run ga8k_hot0_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot0.so; run ga8k_hot1_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot1.so; done ;;
     abeval) run ab_eval 300 python -u tools/ab_eval.py old new ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python -u bench.py --no-pmc --no-cpu --steps 100 ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -9,7 +9,7 @@ the form the library used on the host before round 4), and, where oracle/_ref
 is present, the reference's own Problem(istream&) (its eventCorrelations
 triple loop is O(E^2 S): 108 s at syn in the survey).
 
-    python tools/time_problem.py [out.json] [repeats]
+    python tools/time_problem.py [out.json] [repeats] [configs, comma-separated]
 """
 from __future__ import annotations
 
@@ -34,7 +34,8 @@ def main():
     from oracle_lib import oracle, ref
     O = oracle()
     R = ref()
-    for name in ("med", "lg", "comp01", "syn"):
+    names = sys.argv[3].split(",") if len(sys.argv) > 3 else ["med", "lg", "comp01", "syn"]
+    for name in names:
         inst = ttga.config_instance(name)
         with tempfile.TemporaryDirectory() as d:
             path = pathlib.Path(d) / f"{name}.tim"
