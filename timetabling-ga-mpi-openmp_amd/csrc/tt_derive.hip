@@ -5,7 +5,7 @@
 //
 //   Atb [Ep][Sp/32] u32  event-major BIT image of student_events: bit s of
 //                     event e's row is A[s][e]; Ep = E rounded up to 64, Sp = S
-//                     rounded up to 512, zero padded (derive_layout, built by the
+//                     rounded up to 128, zero padded (derive_layout, built by the
 //                     host from the CSR it needs anyway: one pass over the
 //                     nonzeros). 1.3 MB at syn: the operands stay in L2.
 //   C = At · Atᵀ      C[i][j] = #students attending both i and j; C[i][i] =
@@ -18,9 +18,9 @@
 // expanded in registers to 16 bytes of 0/1 (per nibble x: x·0x00204081 &
 // 0x01010101 puts bit k in byte k), for A (events i) and B (events j) alike,
 // so the k order is the same on both sides. A lane loads 128 students (four
-// steps) of its row with one 16-B load, four such chunks ahead of the MFMAs
-// that use them (the loads are L2 hits; one chunk ahead left the wave waiting
-// on each: 37.5 us at syn). C is symmetric,
+// steps) of its row with one 16-B load, one chunk ahead (four chunks ahead
+// measured 41 us against 37.5 at syn: the waves are bound by the 26 expansion
+// VALU per MFMA, not by the L2 loads). C is symmetric,
 // so an off-diagonal block's quadrant is written twice: its rows (ballots of
 // C > 0 per accumulator register) and its columns (the bits of a lane's own
 // accumulators, the two lane halves OR-ed). The image parts written:
@@ -91,23 +91,14 @@ __global__ __launch_bounds__(256) void derive_corr_kernel(const uint32_t* __rest
     const v4i* pb = (const v4i*)(Atb + (size_t)(j0 + r) * SW);
     const int sh = 16 * h;
     v16i acc = {};
-    constexpr int PD = 4;                                      // chunks in flight (nch is a multiple of PD)
-    v4i ra[PD], rb[PD];
+    v4i na = nch ? pa[0] : v4i{}, nbv = nch ? pb[0] : v4i{};
+    for (int c = 0; c < nch; c++) {                            // the next chunk in flight
+        const v4i wa = na, wb = nbv;
+        if (c + 1 < nch) { na = pa[c + 1]; nbv = pb[c + 1]; }
 #pragma unroll
-    for (int k = 0; k < PD; k++) {
-        ra[k] = k < nch ? pa[k] : v4i{};
-        rb[k] = k < nch ? pb[k] : v4i{};
-    }
-    for (int c = 0; c < nch; c += PD) {
-#pragma unroll
-        for (int k = 0; k < PD; k++) {
-            const v4i wa = ra[k], wb = rb[k];
-            if (c + PD + k < nch) { ra[k] = pa[c + PD + k]; rb[k] = pb[c + PD + k]; }
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(bits_to_bytes((uint32_t)wa[q] >> sh),
-                                                            bits_to_bytes((uint32_t)wb[q] >> sh), acc, 0, 0, 0);
-        }
+        for (int q = 0; q < 4; q++)
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(bits_to_bytes((uint32_t)wa[q] >> sh),
+                                                        bits_to_bytes((uint32_t)wb[q] >> sh), acc, 0, 0, 0);
     }
 
     const int EW = (E + 31) >> 5, EW64 = (E + 63) >> 6;

@@ -247,7 +247,7 @@ __device__ __forceinline__ uint32_t gap_slots4(uint32_t x) {
 }
 __device__ __forceinline__ uint8_t gap_slot(uint32_t s) { return (uint8_t)gap_slots4(s); }
 #ifndef TT_LANES_GAP
-#define TT_LANES_GAP 0
+#define TT_LANES_GAP 1
 #endif
 template <bool GAP>
 __device__ __forceinline__ int mask_terms(uint64_t m) { return GAP ? mask_scv_gap(m) : mask_scv(m); }
@@ -1244,31 +1244,45 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
         if (rc) return rc;
     } else if (variant == 7 || variant == 8) {
         const int NW = variant == 7 ? 4 : 8;
-        // LDS-DMA staging into two tile buffers when rows are 4-B aligned and both
-        // buffers keep 2 workgroups per CU; else one buffer and byte copies
-        const bool db = (E & 3) == 0 && (((uintptr_t)slot) & 3) == 0 && tile5_layout(E, R, NW, true).bytes <= 80 * 1024;
-        const Tile5Layout TL5 = tile5_layout(E, R, NW, db);
-        if (p->dev.EW64 > 7 || TL5.bytes > 160 * 1024 || E > 32767) {
+        // LDS-DMA staging into two tile buffers when rows are 4-B aligned and the
+        // second buffer costs no resident workgroups; else one buffer filled by
+        // vector copies. (With one tile per workgroup the second buffer is never
+        // filled under compute: only the occupancy decides. At med the 8-wave
+        // kernel keeps 2 workgroups per CU either way; the 4-wave kernel fits 4
+        // per CU with one buffer, 2 with two.)
+        const Tile5Layout L0 = tile5_layout(E, R, NW, false), L1 = tile5_layout(E, R, NW, true);
+        const bool db_ok = (E & 3) == 0 && (((uintptr_t)slot) & 3) == 0 && L1.bytes <= 160 * 1024;
+        if (p->dev.EW64 > 7 || L0.bytes > 160 * 1024 || E > 32767) {
             set_error("instance too large for the tile5 kernel");
             return TT_ERR_LIMIT;
         }
         const int max_sn = p->student_number.empty() ? 0 : *std::max_element(p->student_number.begin(), p->student_number.end());
         const int pk = (R <= 16 && max_sn <= 0xFFFF) ? 1 : R <= 32 ? 2 : 0;
         const int tiles = (P + 63) / 64;
-        auto launch = [&](auto kern) -> int {
+        auto occupancy = [&](auto kern, size_t bytes) -> int {
             int per_cu = 0;
-            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, TL5.bytes));
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, bytes) != hipSuccess) return 0;
+            return per_cu;
+        };
+        auto launch = [&](auto kern, size_t bytes) -> int {
+            int per_cu = 0;
+            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, bytes));
             // one tile per workgroup: later workgroups start as earlier ones finish, so a
             // CU's two workgroups drift out of step (one's staging under the other's
             // compute); the persistent grid kept them in lockstep (med -3 %, lg -4 %,
             // P = 262,144 -8 %). ablate 64: the persistent grid (comparison only).
             const int grid = (ablate & 64) ? std::min(tiles, std::max(1, per_cu) * p->num_cus) : tiles;
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NW), TL5.bytes, st, p->dev, slot, room, P, hcv, scv,
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NW), bytes, st, p->dev, slot, room, P, hcv, scv,
                                feasible, penalty, ablate);
             return TT_OK;
         };
-#define TT_T5U(EWC, NWV, PKV) \
-    rc = db ? launch(eval_tile5_kernel<EWC, NWV, PKV, true>) : launch(eval_tile5_kernel<EWC, NWV, PKV, false>);
+#define TT_T5U(EWC, NWV, PKV)                                                                                      \
+    {                                                                                                              \
+        const bool db = db_ok && occupancy(eval_tile5_kernel<EWC, NWV, PKV, true>, L1.bytes) >=                    \
+                                     occupancy(eval_tile5_kernel<EWC, NWV, PKV, false>, L0.bytes);                 \
+        rc = db ? launch(eval_tile5_kernel<EWC, NWV, PKV, true>, L1.bytes)                                         \
+                : launch(eval_tile5_kernel<EWC, NWV, PKV, false>, L0.bytes);                                       \
+    }
 #define TT_T5N(EWC, NWV) \
     if (pk == 1) { TT_T5U(EWC, NWV, 1) } else if (pk == 2) { TT_T5U(EWC, NWV, 2) } else { TT_T5U(EWC, NWV, 0) }
 #define TT_T5(EWC)                                                      \

@@ -56,15 +56,15 @@ int check_pop_args(const tt_problem* p, int P, const void* a, const void* b);
 int use_device(const tt_problem* p);
 
 // Bit image of the attendance matrix for the device derivation: Ep = E rounded
-// up to 64 event rows of SW u32 words, Sp = S rounded up to 512 students (four
-// 128-student chunks per prefetch group).
+// up to 64 event rows of SW u32 words, Sp = S rounded up to 128 students (one
+// 16-B load per lane per chunk).
 struct DeriveLayout {
     int Ep, Sp, SW;
 };
 inline DeriveLayout derive_layout(int E, int S) {
     DeriveLayout L;
     L.Ep = (E + 63) & ~63;
-    L.Sp = (S + 511) & ~511;
+    L.Sp = (S + 127) & ~127;
     L.SW = L.Sp / 32;
     return L;
 }

@@ -783,13 +783,16 @@ __device__ __forceinline__ bool feasible_now(LsState& S) {
     LSP_T(t0);
     int h = 0;
     for (int t = S.lane; t < kSlots; t += 64) h += S.rp[t];
-    for (int e = S.lane; e < S.E; e += 64) {
-        const int t = S.sl[e];
-        int c = 0;
-        for (int w = 0; w < S.EW; ++w) c += __popcll(S.pb.corr64[(size_t)e * S.EW + w] & S.B[(size_t)t * S.EW + w]);
-        c -= (int)((S.pb.corr64[(size_t)e * S.EW + (e >> 6)] >> (e & 63)) & 1ull);
-        h += c;   // every correlated same-slot pair is counted twice, only zero matters
-        h += (int)(((S.pb.poss[e] >> S.rr[e]) & 1ull) ^ 1ull);
+    for (int k = 0; 64 * k < S.E; ++k) {                   // wave-uniform
+        const int e = 64 * k + S.lane;
+        if (e < S.E) {
+            const int t = S.sl[e];
+            int c = 0;
+            for (int w = 0; w < S.EW; ++w) c += __popcll(S.pb.corr64[(size_t)e * S.EW + w] & S.B[(size_t)t * S.EW + w]);
+            c -= (int)((S.pb.corr64[(size_t)e * S.EW + (e >> 6)] >> (e & 63)) & 1ull);
+            h += c;   // every correlated same-slot pair is counted twice, only zero matters
+            h += (int)(((S.pb.poss[e] >> S.rr[e]) & 1ull) ^ 1ull);
+        }
     }
     const bool f = wave_sum(h) == 0;
     LSP_ADD(S, kPfFeas, t0);
@@ -915,8 +918,6 @@ __device__ __forceinline__ uint64_t bperm64(uint64_t v, int src_lane) {
     return ((uint64_t)(uint32_t)bperm((int)(uint32_t)(v >> 32), src_lane) << 32) | (uint32_t)bperm((int)(uint32_t)v, src_lane);
 }
 
-__device__ __forceinline__ bool hot_bit(uint64_t hot, int e) { return (bperm64(hot, e >> 6) >> (e & 63)) & 1ull; }
-
 // Resolves a window of `rem` remaining trials (lanes k < rem) whose per-lane
 // full-path flag is `need`: returns the lane of the first trial to run in
 // full (64: none), with st/step advanced past it (its draw and step taken);
@@ -944,17 +945,22 @@ __device__ __forceinline__ int window_resolve(int lane, uint32_t jump, int64_t& 
 }
 
 // TT_LS_HOT (phase 1): the events with eventHcv > 0 as a bitmask over event
-// ids, one 64-bit word per lane (lane w: events 64w..64w+63). A visit of an
-// event with eventHcv == 0 only counts towards evCount (no draw, no step:
+// ids, one word per lane (lane w: events 64w..64w+63). A visit of an event
+// with eventHcv == 0 only counts towards evCount (no draw, no step:
 // Solution.cpp:509-512), so the visit loop jumps over such events 64 scramble
 // positions at a time instead of loading each one's correlation row. The flags
 // change only for the events of the slots an accepted move touches
-// (eventHcv(e) depends on e's slot only), which refresh_hot recomputes.
+// (eventHcv(e) depends on e's slot only), which refresh_hot recomputes. Used
+// when at most a quarter of the events have eventHcv > 0 at the start of phase 1
+// (a GA child of feasible parents); from a random solution nearly every event
+// is visited anyway and the flags' upkeep after every accepted move only costs.
+// (The flags in LDS instead of a register measured slower: 136 VGPRs spilled.)
 #ifndef TT_LS_HOT
-#define TT_LS_HOT 0
+#define TT_LS_HOT 1
 #endif
-// eventHcv(e) > 0 for events e = 64k + lane; with `all` every event, else only
-// those in a touched slot (S.ts, after accept) replace their flag in `hot`
+// The flags of events 64k + lane; with `all` every event, else
+// only those in a touched slot (S.ts, after accept) replace their flag in `hot`
+// (lane k holds word k)
 __device__ __forceinline__ uint64_t refresh_hot(const LsState& S, uint64_t hot, bool all) {
     const int E = S.E, R = S.R, EW = S.EW, lane = S.lane;
     for (int k = 0; 64 * k < E; ++k) {                        // wave-uniform
@@ -976,6 +982,7 @@ __device__ __forceinline__ uint64_t refresh_hot(const LsState& S, uint64_t hot, 
     }
     return hot;
 }
+
 // One individual's localSearch by the calling wave (every lane). CAP =
 // matcher task capacity. redo_list (first launch, CAP = kLsCapSmall): an
 // individual that overflowed a task is appended to it (redo_list[0] counts,
@@ -1119,8 +1126,13 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
         // TT_LS_ROWPF: the visited event's correlation row loaded one visit ahead
         // (the scrambled event list is fixed, so the next visit's event is known)
         uint64_t nrow = (fast1 && TT_LS_ROWPF) ? load_row(S, S.evl[0]) : 0ull;
-        const bool hotm = TT_LS_HOT && fast1;
-        uint64_t hot = hotm ? refresh_hot(S, 0ull, true) : 0ull;
+        uint64_t hot = 0;
+        int nhot = 0;
+        if (TT_LS_HOT && fast1) {
+            hot = refresh_hot(S, 0ull, true);
+            nhot = wave_sum(lane < EW ? __popcll(hot) : 0);
+        }
+        const bool hotm = TT_LS_HOT && fast1 && 4 * nhot <= E;
         for (int i = 0; evc < E; i = (i + 1) % E) {
             if (step > max_steps || ++guard > guard_max) break;
             if (hotm) {
@@ -1131,7 +1143,9 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                     const int rem = E - evc;                            // visits left before the loop ends
                     int pk = i + lane;
                     while (pk >= E) pk -= E;
-                    const uint64_t hb = ballot(hot_bit(hot, S.evl[pk]) && lane < rem);
+                    const int ek = S.evl[pk];
+                    const uint64_t hw = bperm64(hot, ek >> 6);
+                    const uint64_t hb = ballot(lane < rem && ((hw >> (ek & 63)) & 1ull));
                     if (hb) {
                         const int k = __builtin_ctzll(hb);
                         evc += k; guard += k;
@@ -1206,11 +1220,13 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         if (lb >= c) { S.c1_valid = 1; continue; }
                         LSP_CNT(S, kPfP1m1m);
                         if (match_tasks(S, 1)) goto redo;
-                        if (lb + S.misc[0] < c) { LSP_CNT(S, kPfP1m1a); accept(S); if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
+                        if (lb + S.misc[0] < c) { LSP_CNT(S, kPfP1m1a); accept(S);
+                            if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
                     } else {
                         if (match_tasks(S, 7)) goto redo;
                         const int n = eah_nb(S, ei) + S.misc[task_of(S, t_orig)];
-                        if (n < c) { accept(S); if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
+                        if (n < c) { accept(S);
+                            if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
                     }
                     reject_move1(S);
                 }
@@ -1287,7 +1303,8 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                             if (match_tasks(S, 2, tr)) goto redo;
                         } else if (match_tasks(S, 7, tr)) goto redo;
                         const int n = lb + S.misc[task_of(S, slot_nb(S, ei))] + S.misc[task_of(S, slot_nb(S, ej))];
-                        if (n < c) { accept(S); if (hotm) hot = refresh_hot(S, hot, false); acc = true; break; }
+                        if (n < c) { accept(S);
+                            if (hotm) hot = refresh_hot(S, hot, false); acc = true; break; }
                         sync_rooms(S, false);
                     } while (0);
                     if (acc) { evc = 0; better = true; break; }
@@ -1308,7 +1325,8 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                             set_move(S, 3, ei, ej, ek);
                             if (build_and_match(S)) goto redo;
                             const int n = eah_nb(S, ei) + eah_nb(S, ej) + eah_nb(S, ek);
-                            if (n < c) { accept(S); if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
+                            if (n < c) { accept(S);
+                            if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
                             sync_rooms(S, false);
                         }
                         if (step > max_steps) break;
@@ -1318,7 +1336,8 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                             set_move(S, 3, ei, ek, ej);
                             if (build_and_match(S)) goto redo;
                             const int n = eah_nb(S, ei) + eah_nb(S, ek) + eah_nb(S, ej);
-                            if (n < c) { accept(S); if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
+                            if (n < c) { accept(S);
+                            if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
                             sync_rooms(S, false);
                         }
                     }

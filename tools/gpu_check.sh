@@ -77,11 +77,12 @@ for s in $STEPS; do
     pmcga) pmc pmc_ga local_search_kernel python -u tools/bench_ga.py $GA8K --gens 10 --cpu-sample 0 ;;
     pmcwide) pmc pmc_wide eval_ python -u tools/eval_variants.py syn 65536 13 ;;
     abls)  run ab_comp01 400 python -u tools/ab_ls.py comp01 8192 old new && run ab_med 400 python -u tools/ab_ls.py med 4096 old new ;;
-    stamps) run t5_stamps 300 python -u tools/t5_stamps.py ;;
+    stamps) run t5_stamps 300 python -u tools/t5_stamps.py --raw "$OUT/t5_stamps_raw.npz" ;;
     replace) run time_replace 300 python -u tools/time_replace.py ;;
     ablanes) run ab_lanes 400 python -u tools/ab_eval.py syn 262144 gap0:13 gap1:13 gap0:77 gap1:77 ;;
-    abhot) run ab_hot_comp01 400 python -u tools/ab_ls.py comp01 8192 hot0 hot1 && run ab_hot_med 400 python -u tools/ab_ls.py med 4096 hot0 hot1 ;;
-    gahot) for i in 1 2; do run ga8k_hot0_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot0.so; run ga8k_hot1_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot1.so; done ;;
+    abhot) run ab_hot_comp01 400 python -u tools/ab_ls.py comp01 8192 hot0 hot1 hot2 && run ab_hot_med 400 python -u tools/ab_ls.py med 4096 hot0 hot1 hot2 ;;
+    gahot) for i in 1 2; do run ga8k_hot0_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot0.so; run ga8k_hot1_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot1.so; run ga8k_hot2_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot2.so; done ;;
+    abocc) run ab_occ_med 300 python -u tools/ab_eval.py med 65536 t5old:8 t5old:7 occ:8 occ:7 && run ab_occ_lg 300 python -u tools/ab_eval.py lg 65536 t5old:8 t5old:7 occ:8 occ:7 && run ab_occ_comp01 300 python -u tools/ab_eval.py comp01 65536 t5old:8 occ:8 occ:7 ;;
     abeval) run ab_eval 300 python -u tools/ab_eval.py old new ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python -u bench.py --no-pmc --no-cpu --steps 100 ;;
     *) echo "unknown step $s"; exit 2 ;;
