@@ -38,7 +38,7 @@ pmc() {
         timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d "$OUT/$name/pmc$i" -o pmc -- "$@" \
             > "$OUT/$name.pmc$i.log" 2>&1 || { echo "pmc pass $i rc=$?"; exit 125; }
     done
-    python tools/pmc_summary.py "$OUT/$name" "$kernel" > "$OUT/$name.json"; cat "$OUT/$name.json"
+    python tools/pmc_summary.py "$OUT/$name" "$kernel" ${PMC_LAST:+--last $PMC_LAST} > "$OUT/$name.json"; cat "$OUT/$name.json"
 }
 GA8K="--config comp01 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6"
 for s in $STEPS; do
@@ -59,7 +59,7 @@ for s in $STEPS; do
     ga8k)  run ga8k 400 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 512 ;;
     ga32k) run ga32k 300 python -u tools/bench_ga.py --config comp01 --pop 65536 --children 32768 --gens 10 --min-seconds 1.0 --steps 1000 --warm-gens 30 --warm-feasible 0.6 --cpu-sample 0 ;;
     gatrace) run ga8k_trace 400 rocprofv3 --kernel-trace --stats -d "$OUT/ga_trace" -o run --output-format csv -- python -u tools/bench_ga.py $GA8K --gens 20 --cpu-sample 0 ;;
-    lsprof) run lsprof_ga 300 python -u tools/ls_prof.py --config comp01 --pop 65536 --children 8192 --from-ga 0.6 --steps 1000 ;;
+    lsprof) run lsprof_ga 300 python -u tools/ls_prof.py --config comp01 --pop 65536 --children 8192 --from-ga 0.999 --steps 1000 ;;
     timeprob) run time_problem 600 python -u tools/time_problem.py "$OUT/time_problem.json" 5 ;;
     profderive) run rocprof_derive 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_derive" -o run --output-format csv -- python -u tools/time_problem.py "$OUT/time_problem_traced.json" 5 ;;
     pmcderive)
@@ -74,7 +74,7 @@ for s in $STEPS; do
     pmc3)  run pmc3 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc3" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
     pmc4)  run pmc4 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc4" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
     pmcls) pmc pmc_ls local_search_kernel python -u tools/bench_ls.py --cpu-sample 0 --reps 1 --pop 4096 --steps 1000 --pre-steps 3000 ;;
-    pmcga) pmc pmc_ga local_search_kernel python -u tools/bench_ga.py $GA8K --gens 10 --cpu-sample 0 ;;
+    pmcga) PMC_LAST=10 pmc pmc_ga local_search_kernel python -u tools/bench_ga.py --config comp01 --pop 65536 --children 8192 --steps 1000 --warm-gens 400 --warm-feasible 0.999 --gens 10 --cpu-sample 0 ;;
     pmcwide) pmc pmc_wide eval_ python -u tools/eval_variants.py syn 65536 13 ;;
     abls)  run ab_comp01 400 python -u tools/ab_ls.py comp01 8192 old new && run ab_med 400 python -u tools/ab_ls.py med 4096 old new ;;
     stamps) run t5_stamps 300 python -u tools/t5_stamps.py --raw "$OUT/t5_stamps_raw.npz" ;;
