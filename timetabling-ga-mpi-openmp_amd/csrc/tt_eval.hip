@@ -668,7 +668,8 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
         }
     }
 #ifdef TT_T5_STAMP
-    if ((threadIdx.x & 63) == 0) st_rec[2 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) < kT5Words - 2)
+        st_rec[2 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
 
@@ -1243,6 +1244,9 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
                  : NB == 4 ? launch(eval_corr_kernel<4, kCorrMaxEPL>) : launch(eval_corr_kernel<2, kCorrMaxEPL>);
         if (rc) return rc;
     } else if (variant == 7 || variant == 8) {
+        // 4 or 8 waves per tile, one tile per workgroup. (16 waves, one workgroup per CU
+        // looping over its tiles with the next one staged under the current one: med
+        // 82.0 us against 76.0, lg 106.2 against 99.8 -- measured in round 4, removed.)
         const int NW = variant == 7 ? 4 : 8;
         // LDS-DMA staging into two tile buffers when rows are 4-B aligned and the
         // second buffer costs no resident workgroups; else one buffer filled by

@@ -34,7 +34,7 @@ constexpr int kLsCapSmall = 64;
 // Profiling build (-DTT_LS_PROF, `make libttga_prof.so`, tools/ls_prof.py):
 // per-section shader-clock totals of every wave, summed into g_ls_prof.
 #ifdef TT_LS_PROF
-enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfQ1, kPfQ1c, kPfQ1m, kPfQ2, kPfQ2c, kPfQ2m, kPfP1m2, kPfP1m2lb, kPfP1m1m, kPfP1m1a, kPfP1m1k, kPfVis1, kPfM1p1, kPfM2p1, kPfPh1, kPfPh2, kPfVis2, kPfM1p2, kPfM2p2, kPfMaxTotal, kPfN };
+enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfQ1, kPfQ1c, kPfQ1m, kPfQ2, kPfQ2c, kPfQ2m, kPfP1m2, kPfP1m2lb, kPfP1m1m, kPfP1m1a, kPfP1m1k, kPfVis1, kPfM1p1, kPfM2p1, kPfPh1, kPfPh2, kPfVis2, kPfM1p2, kPfM2p2, kPfSkip1, kPfHot1, kPfMaxTotal, kPfN };
 __device__ unsigned long long g_ls_prof[kPfN];
 #define LSP_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define LSP_ADD(St, i, v) ((St).prof[i] += __builtin_amdgcn_s_memtime() - (v))
@@ -961,7 +961,8 @@ __device__ __forceinline__ int window_resolve(int lane, uint32_t jump, int64_t& 
 // The flags of events 64k + lane; with `all` every event, else
 // only those in a touched slot (S.ts, after accept) replace their flag in `hot`
 // (lane k holds word k)
-__device__ __forceinline__ uint64_t refresh_hot(const LsState& S, uint64_t hot, bool all) {
+__device__ __forceinline__ uint64_t refresh_hot(LsState& S, uint64_t hot, bool all) {
+    LSP_T(t0);
     const int E = S.E, R = S.R, EW = S.EW, lane = S.lane;
     for (int k = 0; 64 * k < E; ++k) {                        // wave-uniform
         const int e = 64 * k + lane;
@@ -980,6 +981,7 @@ __device__ __forceinline__ uint64_t refresh_hot(const LsState& S, uint64_t hot, 
         const uint64_t um = ballot(upd), hm = ballot(h);
         if (um && lane == k) hot = (hot & ~um) | hm;
     }
+    LSP_ADD(S, kPfHot1, t0);
     return hot;
 }
 
@@ -1136,6 +1138,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
         for (int i = 0; evc < E; i = (i + 1) % E) {
             if (step > max_steps || ++guard > guard_max) break;
             if (hotm) {
+                LSP_T(t_skip);
                 // jump to the next event with eventHcv > 0 (each one skipped is a visit
                 // that only counts towards evCount); the loop ends after E in a row
                 bool out = false;
@@ -1157,6 +1160,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                     i = (i + n) % E;
                     if (evc >= E) { out = true; break; }
                 }
+                LSP_ADD(S, kPfSkip1, t_skip);
                 if (out || guard > guard_max) break;
             }
             const int ei = S.evl[i];

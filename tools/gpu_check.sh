@@ -40,6 +40,13 @@ pmc() {
     done
     python tools/pmc_summary.py "$OUT/$name" "$kernel" ${PMC_LAST:+--last $PMC_LAST} > "$OUT/$name.json"; cat "$OUT/$name.json"
 }
+# the profiling library (make prof) must be newer than every source it is built from
+prof_fresh() {
+    local lib=timetabling-ga-mpi-openmp_amd/libttga_prof.so
+    if [ ! -f "$lib" ] || [ -n "$(find timetabling-ga-mpi-openmp_amd/csrc include -newer "$lib" -type f)" ]; then
+        echo "stale $lib: run make -C timetabling-ga-mpi-openmp_amd prof"; exit 2
+    fi
+}
 GA8K="--config comp01 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6"
 for s in $STEPS; do
   case $s in
@@ -59,7 +66,7 @@ for s in $STEPS; do
     ga8k)  run ga8k 400 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 512 ;;
     ga32k) run ga32k 300 python -u tools/bench_ga.py --config comp01 --pop 65536 --children 32768 --gens 10 --min-seconds 1.0 --steps 1000 --warm-gens 30 --warm-feasible 0.6 --cpu-sample 0 ;;
     gatrace) run ga8k_trace 400 rocprofv3 --kernel-trace --stats -d "$OUT/ga_trace" -o run --output-format csv -- python -u tools/bench_ga.py $GA8K --gens 20 --cpu-sample 0 ;;
-    lsprof) run lsprof_ga 300 python -u tools/ls_prof.py --config comp01 --pop 65536 --children 8192 --from-ga 0.999 --steps 1000 ;;
+    lsprof) prof_fresh; run lsprof_ga 300 python -u tools/ls_prof.py --config comp01 --pop 65536 --children 8192 --from-ga 0.999 --steps 1000 ;;
     timeprob) run time_problem 600 python -u tools/time_problem.py "$OUT/time_problem.json" 5 ;;
     profderive) run rocprof_derive 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_derive" -o run --output-format csv -- python -u tools/time_problem.py "$OUT/time_problem_traced.json" 5 ;;
     pmcderive)
@@ -77,7 +84,7 @@ for s in $STEPS; do
     pmcga) PMC_LAST=10 pmc pmc_ga local_search_kernel python -u tools/bench_ga.py --config comp01 --pop 65536 --children 8192 --steps 1000 --warm-gens 400 --warm-feasible 0.999 --gens 10 --cpu-sample 0 ;;
     pmcwide) pmc pmc_wide eval_ python -u tools/eval_variants.py syn 65536 13 ;;
     abls)  run ab_comp01 400 python -u tools/ab_ls.py comp01 8192 old new && run ab_med 400 python -u tools/ab_ls.py med 4096 old new ;;
-    stamps) run t5_stamps 300 python -u tools/t5_stamps.py --raw "$OUT/t5_stamps_raw.npz" ;;
+    stamps) prof_fresh; run t5_stamps 300 python -u tools/t5_stamps.py --raw "$OUT/t5_stamps_raw.npz" ;;
     replace) run time_replace 300 python -u tools/time_replace.py ;;
     ablanes) run ab_lanes 400 python -u tools/ab_eval.py syn 262144 gap0:13 gap1:13 gap0:77 gap1:77 ;;
     abhot) run ab_hot_comp01 400 python -u tools/ab_ls.py comp01 8192 hot0 hot1 hot2 && run ab_hot_med 400 python -u tools/ab_ls.py med 4096 hot0 hot1 hot2 ;;

@@ -71,7 +71,7 @@ torch.cuda.synchronize()
 ev_ms = e0.elapsed_time(e1) / L
 lib.tt_t5_stamp_read(buf.ctypes.data, 0)
 grid = (P + 63) // 64
-nw = 8 if a.variant == 8 else 4
+nw = 4 if a.variant == 7 else 8                   # stamped waves (at most 8)
 st = buf.reshape(NL, NB, NWD).astype(np.int64)[:L, :grid]
 if a.raw:
     np.savez_compressed(a.raw, stamps=st)
