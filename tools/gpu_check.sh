@@ -82,7 +82,8 @@ for s in $STEPS; do
     pmc4)  run pmc4 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc4" -o pmc -- python -u bench.py --no-pmc --no-cpu --steps 3 --warmup 1 ;;
     pmcls) pmc pmc_ls local_search_kernel python -u tools/bench_ls.py --cpu-sample 0 --reps 1 --pop 4096 --steps 1000 --pre-steps 3000 ;;
     pmcga) PMC_LAST=10 pmc pmc_ga local_search_kernel python -u tools/bench_ga.py --config comp01 --pop 65536 --children 8192 --steps 1000 --warm-gens 400 --warm-feasible 0.999 --gens 10 --cpu-sample 0 ;;
-    pmcwide) pmc pmc_wide eval_ python -u tools/eval_variants.py syn 65536 13 ;;
+    pmcwide) pmc pmc_wide eval_lanes python -u tools/eval_variants.py syn 65536 13 &&
+             python tools/pmc_summary.py "$OUT/pmc_wide" eval_corr > "$OUT/pmc_wide_corr.json" ;;
     abls)  run ab_comp01 400 python -u tools/ab_ls.py comp01 8192 old new && run ab_med 400 python -u tools/ab_ls.py med 4096 old new ;;
     stamps) prof_fresh; run t5_stamps 300 python -u tools/t5_stamps.py --raw "$OUT/t5_stamps_raw.npz" ;;
     replace) run time_replace 300 python -u tools/time_replace.py ;;
