@@ -92,6 +92,7 @@ for s in $STEPS; do
     gahot) for i in 1 2; do run ga8k_hot0_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot0.so; run ga8k_hot1_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot1.so; run ga8k_hot2_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot2.so; done ;;
     abocc) run ab_occ_med 300 python -u tools/ab_eval.py med 65536 t5old:8 t5old:7 occ:8 occ:7 && run ab_occ_lg 300 python -u tools/ab_eval.py lg 65536 t5old:8 t5old:7 occ:8 occ:7 && run ab_occ_comp01 300 python -u tools/ab_eval.py comp01 65536 t5old:8 occ:8 occ:7 ;;
     abeval) run ab_eval 300 python -u tools/ab_eval.py old new ;;
+    gaab) for i in 1 2; do for l in old new; do run ga8k_${l}_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python -u bench.py --no-pmc --no-cpu --steps 100 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
