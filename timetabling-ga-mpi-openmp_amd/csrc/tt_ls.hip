@@ -944,6 +944,14 @@ __device__ __forceinline__ int window_resolve(int lane, uint32_t jump, int64_t& 
     return kstar;
 }
 
+// x mod E for 0 <= x < E + 64 (scramble positions a window ahead): a subtraction
+// or two instead of the integer division a runtime `% E` compiles to (dozens of
+// scalar or vector instructions per use in the trial loops)
+__device__ __forceinline__ int wrap_e(int x, int E) {
+    while (x >= E) x -= E;
+    return x;
+}
+
 // TT_LS_HOT (phase 1): the events with eventHcv > 0 as a bitmask over event
 // ids, one word per lane (lane w: events 64w..64w+63). A visit of an event
 // with eventHcv == 0 only counts towards evCount (no draw, no step:
@@ -1135,7 +1143,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
             nhot = wave_sum(lane < EW ? __popcll(hot) : 0);
         }
         const bool hotm = TT_LS_HOT && fast1 && 4 * nhot <= E;
-        for (int i = 0; evc < E; i = (i + 1) % E) {
+        for (int i = 0; evc < E; i = wrap_e(i + 1, E)) {
             if (step > max_steps || ++guard > guard_max) break;
             if (hotm) {
                 LSP_T(t_skip);
@@ -1152,12 +1160,12 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                     if (hb) {
                         const int k = __builtin_ctzll(hb);
                         evc += k; guard += k;
-                        i = (i + k) % E;
+                        i = wrap_e(i + k, E);
                         break;
                     }
                     const int n = rem < 64 ? rem : 64;
                     evc += n; guard += n;
-                    i = (i + n) % E;
+                    i = wrap_e(i + n, E);
                     if (evc >= E) { out = true; break; }
                 }
                 LSP_ADD(S, kPfSkip1, t_skip);
@@ -1246,13 +1254,13 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                     bo = S.B[(size_t)t_orig * EW + lane];
                     if ((ei >> 6) == lane) bo &= ~(1ull << (ei & 63));
                 }
-                int j = (i + 1) % E;
+                int j = wrap_e(i + 1, E);
                 while (j != i) {
                     if (step > max_steps) break;
                     if (fast1 && (uint64_t)st < kPmM) {
                         // window: lane k screens trial j+k against the lower bound
                         // lb = corr_nb(ei) + corr_nb(ej) >= c = eah_i + eah_cur(ej)
-                        const int rem = (i - j + E) % E;
+                        const int rem = wrap_e(i - j + E, E);
                         // (ds_bpermute reads 0 from inactive lanes: every lane takes part)
 #if TT_LS_SLP
                         int pk = j + lane;
@@ -1260,7 +1268,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         if (pk >= E) pk %= E;                      // E < 64 only
                         const int ej = S.evl[pk], tj = S.slp[pk];
 #else
-                        const int ej = S.evl[(j + lane) % E], tj = S.sl[ej];
+                        const int ej = S.evl[wrap_e(j + lane, E)], tj = S.sl[ej];
 #endif
                         const int xt = bperm(V.x, tj);
                         bool need = true;
@@ -1281,12 +1289,12 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         const int ks = window_resolve(lane, jump, st, step, max_steps, rem, p2, need, done);
                         if (ks == 64) {
                             if (done) break;
-                            j = (j + 64) % E;
+                            j = wrap_e(j + 64, E);
                             continue;
                         }
-                        j = (j + ks) % E;
+                        j = wrap_e(j + ks, E);
                     } else {
-                        if (!(pm_next(st) < p2)) { j = (j + 1) % E; continue; }
+                        if (!(pm_next(st) < p2)) { j = wrap_e(j + 1, E); continue; }
                         step++;
                     }
                     // ---- the full trial at j (its draw and step taken)
@@ -1312,15 +1320,15 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         sync_rooms(S, false);
                     } while (0);
                     if (acc) { evc = 0; better = true; break; }
-                    j = (j + 1) % E;
+                    j = wrap_e(j + 1, E);
                 }
                 LSP_ADD(S, kPfM2p1, t_m2);
                 if (better) { better = false; continue; }
             }
             if (p3 != 0) {
-                for (int j = (i + 1) % E; j != i; j = (j + 1) % E) {
+                for (int j = wrap_e(i + 1, E); j != i; j = wrap_e(j + 1, E)) {
                     if (step > max_steps) break;
-                    for (int k = (j + 1) % E; k != i; k = (k + 1) % E) {
+                    for (int k = wrap_e(j + 1, E); k != i; k = wrap_e(k + 1, E)) {
                         if (step > max_steps) break;
                         const int ej = S.evl[j], ek = S.evl[k];
                         if (pm_next(st) < p3) {
@@ -1372,7 +1380,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
         const bool fast = fast1;
         evc = 0;
         uint64_t nrow = (fast && TT_LS_ROWPF) ? load_row(S, S.evl[0]) : 0ull;
-        for (int i = 0; evc < E; i = (i + 1) % E) {
+        for (int i = 0; evc < E; i = wrap_e(i + 1, E)) {
             if (step > max_steps || ++guard > guard_max) break;
             const int ei = S.evl[i];
             LSP_CNT(S, kPfVisits);
@@ -1439,13 +1447,13 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
             if (p2 != 0) {
                 LSP_T(t_m2);
                 if (fast) visit2_z(S, ei, V);
-                int j = (i + 1) % E;
+                int j = wrap_e(i + 1, E);
                 while (j != i) {
                     if (step > max_steps) break;
                     if (fast && (uint64_t)st < kPmM) {
                         // window: lane k screens partner j+k (no correlated event for either
                         // moved event in its new slot)
-                        const int rem = (i - j + E) % E;
+                        const int rem = wrap_e(i - j + E, E);
                         // (ds_bpermute reads 0 from inactive lanes: every lane takes part)
 #if TT_LS_SLP
                         int pk = j + lane;
@@ -1453,7 +1461,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         if (pk >= E) pk %= E;                      // E < 64 only
                         const int ej = S.evl[pk], tj = S.slp[pk];
 #else
-                        const int ej = S.evl[(j + lane) % E], tj = S.sl[ej];
+                        const int ej = S.evl[wrap_e(j + lane, E)], tj = S.sl[ej];
 #endif
                         const uint64_t rw = bperm64(V.row, ej >> 6), zw = bperm64(V.z, ej >> 6);
                         const int xt = bperm(V.x, tj);
@@ -1466,12 +1474,12 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         const int ks = window_resolve(lane, jump, st, step, max_steps, rem, p2, need, done);
                         if (ks == 64) {
                             if (done) break;
-                            j = (j + 64) % E;
+                            j = wrap_e(j + 64, E);
                             continue;
                         }
-                        j = (j + ks) % E;
+                        j = wrap_e(j + ks, E);
                     } else {
-                        if (!(pm_next(st) < p2)) { j = (j + 1) % E; continue; }
+                        if (!(pm_next(st) < p2)) { j = wrap_e(j + 1, E); continue; }
                         step++;
                     }
                     // ---- the full trial at j (its draw and step taken)
@@ -1510,15 +1518,15 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         sync_rooms(S, false);
                     } while (0);
                     if (acc) { evc = 0; better = true; break; }
-                    j = (j + 1) % E;
+                    j = wrap_e(j + 1, E);
                 }
                 LSP_ADD(S, kPfM2p2, t_m2);
                 if (better) { better = false; continue; }
             }
             if (p3 != 0) {
-                for (int j = (i + 1) % E; j != i; j = (j + 1) % E) {
+                for (int j = wrap_e(i + 1, E); j != i; j = wrap_e(j + 1, E)) {
                     if (step > max_steps) break;
-                    for (int k = (j + 1) % E; k != i; k = (k + 1) % E) {
+                    for (int k = wrap_e(j + 1, E); k != i; k = wrap_e(k + 1, E)) {
                         if (step > max_steps) break;
                         const int ej = S.evl[j], ek = S.evl[k];
                         for (int order = 0; order < 2; ++order) {
