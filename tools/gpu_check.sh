@@ -92,6 +92,10 @@ for s in $STEPS; do
     gahot) for i in 1 2; do run ga8k_hot0_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot0.so; run ga8k_hot1_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot1.so; run ga8k_hot2_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot2.so; done ;;
     abocc) run ab_occ_med 300 python -u tools/ab_eval.py med 65536 t5old:8 t5old:7 occ:8 occ:7 && run ab_occ_lg 300 python -u tools/ab_eval.py lg 65536 t5old:8 t5old:7 occ:8 occ:7 && run ab_occ_comp01 300 python -u tools/ab_eval.py comp01 65536 t5old:8 occ:8 occ:7 ;;
     abeval) run ab_eval 300 python -u tools/ab_eval.py old new ;;
+    abcorr) run ab_corr_syn 400 python -u tools/ab_eval.py syn 262144 old:13 new:13 && run ab_corr_med 300 python -u tools/ab_eval.py med 65536 old:8 new:8 ;;
+    valurate) run valu_rate 120 tools/valu_rate ;;
+    abls4) run ab4_comp01 400 python -u tools/ab_ls.py comp01 8192 old new noscv norow && run ab4_med 400 python -u tools/ab_ls.py med 4096 old new noscv norow ;;
+    gaab4) for i in 1 2; do for l in old new noscv norow; do run ga8k_${l}_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done ;;
     gaab) for i in 1 2; do for l in old new; do run ga8k_${l}_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python -u bench.py --no-pmc --no-cpu --steps 100 ;;
     *) echo "unknown step $s"; exit 2 ;;
