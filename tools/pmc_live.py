@@ -16,7 +16,10 @@ Per launch of the dominant kernel (median over its dispatches):
               streaming read on gfx950; other widths are uncalibrated);
   lds_busy  = SQ_LDS_IDX_ACTIVE / (CUs * GRBM_GUI_ACTIVE / XCDs)  (LDS-array cycles)
   lds_conflict = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
-  valu_busy = 2 * SQ_INSTS_VALU / (4 * CUs * GRBM_GUI_ACTIVE / XCDs)  (wave64 VALU = 2 cycles on a SIMD32)
+  valu_busy = 4 * SQ_INSTS_VALU / (4 * CUs * GRBM_GUI_ACTIVE / XCDs)  (a wave64 VALU instruction
+              occupies its SIMD 4 cycles: tools/valu_rate measured 0.88-0.95
+              wave-instructions per CU-cycle for 32- and 64-bit opcodes; until
+              round 4 this used 2 cycles and reported half the busy fraction)
   salu_busy = SQ_INSTS_SALU / (CUs * GRBM_GUI_ACTIVE / XCDs)      (one scalar unit per CU)
   wait_any  = SQ_WAIT_ANY / SQ_WAVE_CYCLES
 """
@@ -129,7 +132,7 @@ def derive(c: dict | None, calib_bytes: float | None = None) -> dict | None:
             res["lds_busy"] = c["SQ_LDS_IDX_ACTIVE"] / (CUS * cyc)
             res["lds_conflict"] = c.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(c["SQ_LDS_IDX_ACTIVE"], 1.0)
         if "SQ_INSTS_VALU" in c:
-            res["valu_busy"] = 2.0 * c["SQ_INSTS_VALU"] / (4 * CUS * cyc)
+            res["valu_busy"] = 4.0 * c["SQ_INSTS_VALU"] / (4 * CUS * cyc)
         if "SQ_INSTS_SALU" in c:
             res["salu_busy"] = c["SQ_INSTS_SALU"] / (CUS * cyc)
         if "SQ_WAIT_ANY" in c and c.get("SQ_WAVE_CYCLES"):
