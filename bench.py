@@ -252,15 +252,26 @@ def main():
                                                             "wait_any", "cycles") if k in pmc}
             raw = pmc.get("raw", {})
             if "SQ_LDS_IDX_ACTIVE" in raw and pmc.get("cycles"):
-                # the unit that binds these kernels is the LDS (and the issue around it), not HBM:
-                # LDS-array cycles per individual against one LDS cycle per CU per shader cycle
+                # the units that bind these kernels are the VALU and the LDS (and the issue
+                # around them), not HBM: each unit's busy cycles against its issue peak --
+                # one LDS-array cycle per CU per shader cycle, and 4 SIMD cycles per wave64
+                # VALU instruction (one per CU per cycle: tools/valu_rate) -- the busier one
+                # is the binding unit
                 clk = pmc["cycles"] / (kernel_ms * 1e-3)
+                units = {"lds": {"cycles_per_individual": raw["SQ_LDS_IDX_ACTIVE"] / P,
+                                 "frac": pmc.get("lds_busy"), "bank_conflict_share": pmc.get("lds_conflict"),
+                                 "only_us": raw["SQ_LDS_IDX_ACTIVE"] / (256 * clk) * 1e6,
+                                 "peak": "1 LDS-array cycle per CU per shader cycle (MI355X_MICROARCH.md §LDS)"}}
+                if "SQ_INSTS_VALU" in raw:
+                    units["valu"] = {"instructions_per_individual": raw["SQ_INSTS_VALU"] / P,
+                                     "frac": pmc.get("valu_busy"),
+                                     "only_us": raw["SQ_INSTS_VALU"] / (256 * clk) * 1e6,
+                                     "peak": "1 wave64 VALU instruction per CU per shader cycle (4 SIMDs x 4 cycles; "
+                                             "tools/valu_rate, profiles/r04_j_valu_rate.json)"}
+                bind = max(units, key=lambda k: units[k]["frac"] or 0.0)
                 line["roofline"]["binding_unit"] = {
-                    "unit": "LDS-array cycles (SQ_LDS_IDX_ACTIVE, live pass)",
+                    "unit": bind, "frac": units[bind]["frac"], "units": units,
                     "lds_cycles_per_individual": raw["SQ_LDS_IDX_ACTIVE"] / P,
-                    "peak": "1 LDS-array cycle per CU per shader cycle (MI355X_MICROARCH.md §LDS)",
-                    "frac": pmc.get("lds_busy"), "bank_conflict_share": pmc.get("lds_conflict"),
-                    "lds_only_us": raw["SQ_LDS_IDX_ACTIVE"] / (256 * clk) * 1e6,
                     "valu_frac": pmc.get("valu_busy"), "salu_frac": pmc.get("salu_busy"),
                     "clock_ghz": clk / 1e9}
         if variant == 13 and not args.pmc_child:

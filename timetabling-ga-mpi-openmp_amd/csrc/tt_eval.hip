@@ -1260,17 +1260,21 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
             set_error("instance too large for the tile5 kernel");
             return TT_ERR_LIMIT;
         }
-        const int max_sn = p->student_number.empty() ? 0 : *std::max_element(p->student_number.begin(), p->student_number.end());
+        const int max_sn = p->max_sn;
         const int pk = (R <= 16 && max_sn <= 0xFFFF) ? 1 : R <= 32 ? 2 : 0;
         const int tiles = (P + 63) / 64;
-        auto occupancy = [&](auto kern, size_t bytes) -> int {
-            int per_cu = 0;
+        // workgroups per CU of the kernel with one or two tile buffers: asked once per
+        // problem (the occupancy query costs host time on every launch otherwise)
+        auto occupancy = [&](auto kern, size_t bytes, bool two) -> int {
+            std::atomic<int>& c = const_cast<tt_problem*>(p)->t5_occ[NW == 8][two];
+            int per_cu = c.load(std::memory_order_relaxed);
+            if (per_cu >= 0) return per_cu;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, bytes) != hipSuccess) return 0;
+            c.store(per_cu, std::memory_order_relaxed);
             return per_cu;
         };
-        auto launch = [&](auto kern, size_t bytes) -> int {
-            int per_cu = 0;
-            TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, bytes));
+        auto launch = [&](auto kern, size_t bytes, bool two) -> int {
+            const int per_cu = occupancy(kern, bytes, two);
             // one tile per workgroup: later workgroups start as earlier ones finish, so a
             // CU's two workgroups drift out of step (one's staging under the other's
             // compute); the persistent grid kept them in lockstep (med -3 %, lg -4 %,
@@ -1282,10 +1286,10 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
         };
 #define TT_T5U(EWC, NWV, PKV)                                                                                      \
     {                                                                                                              \
-        const bool db = db_ok && occupancy(eval_tile5_kernel<EWC, NWV, PKV, true>, L1.bytes) >=                    \
-                                     occupancy(eval_tile5_kernel<EWC, NWV, PKV, false>, L0.bytes);                 \
-        rc = db ? launch(eval_tile5_kernel<EWC, NWV, PKV, true>, L1.bytes)                                         \
-                : launch(eval_tile5_kernel<EWC, NWV, PKV, false>, L0.bytes);                                       \
+        const bool db = db_ok && occupancy(eval_tile5_kernel<EWC, NWV, PKV, true>, L1.bytes, true) >=              \
+                                     occupancy(eval_tile5_kernel<EWC, NWV, PKV, false>, L0.bytes, false);          \
+        rc = db ? launch(eval_tile5_kernel<EWC, NWV, PKV, true>, L1.bytes, true)                                   \
+                : launch(eval_tile5_kernel<EWC, NWV, PKV, false>, L0.bytes, false);                                \
     }
 #define TT_T5N(EWC, NWV) \
     if (pk == 1) { TT_T5U(EWC, NWV, 1) } else if (pk == 2) { TT_T5U(EWC, NWV, 2) } else { TT_T5U(EWC, NWV, 0) }

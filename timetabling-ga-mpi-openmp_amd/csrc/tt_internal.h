@@ -34,6 +34,11 @@ struct tt_problem {
     // students with phase-2 masks in the local search, per matcher-task cap
     // (full, small); -1 until the first call decides (tt_ls.hip ls_mask_students)
     std::atomic<int> ls_smask[2] = {-1, -1};
+    // eval_tile5 launch decisions, per wave count (4, 8) and tile buffers (1, 2):
+    // workgroups per CU, -1 until the first launch asks (tt_eval.hip); and the
+    // largest studentNumber (packing choice), set at creation
+    std::atomic<int> t5_occ[2][2] = {{-1, -1}, {-1, -1}};
+    int max_sn = 0;
 };
 
 namespace ttga {

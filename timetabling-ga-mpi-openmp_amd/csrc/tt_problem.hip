@@ -227,6 +227,8 @@ int tt_problem_create(int E, int R, int F, int S, const int32_t* room_size, cons
     if (rc == TT_OK) rc = check_hip(hipMemcpy(p->student_number.data(), d.sn, sizeof(int32_t) * E, hipMemcpyDeviceToHost), "tt_problem_create readback");
     if (rc == TT_OK) rc = check_hip(hipMemcpy(p->poss_bits.data(), d.poss, sizeof(uint64_t) * E, hipMemcpyDeviceToHost), "tt_problem_create readback");
     if (rc == TT_OK) rc = check_hip(hipMemcpy(p->corr_bits.data(), d.corr, sizeof(uint32_t) * E * EW, hipMemcpyDeviceToHost), "tt_problem_create readback");
+    if (rc == TT_OK && !p->student_number.empty())
+        p->max_sn = *std::max_element(p->student_number.begin(), p->student_number.end());
     if (rc == TT_OK && p->student_number != degree) {
         set_error("tt_problem_create: device studentNumber differs from the attendance counts");
         rc = TT_ERR_DEVICE;
