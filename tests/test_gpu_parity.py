@@ -375,6 +375,52 @@ def test_local_search_phase2_vs_oracle(orc, p1, p2):
     assert dp.status() == 0
 
 
+def _hot_events(inst, s, r):
+    """Per individual: events with eventHcv > 0 (Solution.cpp:173-191: room
+    clashes in its slot and room plus correlated events in its slot)."""
+    A = inst.student_events.astype(np.int64)
+    C = (A.T @ A) > 0
+    np.fill_diagonal(C, False)
+    out = []
+    for sl, rm in zip(s, r):
+        same_slot = sl[:, None] == sl[None, :]
+        clash = same_slot & (rm[:, None] == rm[None, :])
+        np.fill_diagonal(clash, False)
+        out.append(int(((clash | (C & same_slot)).any(axis=1)).sum()))
+    return np.array(out)
+
+
+def test_local_search_flagged_events_vs_oracle(orc):
+    """GA-child-like starts: feasible individuals with one to three events moved
+    to random slots, so only a few events have eventHcv > 0 and phase 1 visits
+    them through the eventHcv flags (TT_LS_HOT: the unflagged events skipped 64
+    scramble positions at a time, the flags refreshed after every accepted move).
+    Slots, rooms and RNG states identical to the oracle's localSearch."""
+    inst = ttga.generate(300, 12, 4, 150, seed=31)
+    dp = native.DeviceProblem(inst)
+    o = orc.problem(inst)
+    P = 48
+    s0, r0, _ = o.random_init(ttga.population_seeds(2201, P))
+    s1, r1, _ = o.local_search(s0, r0, ttga.population_seeds(2301, P), 3000)
+    feas = o.eval(s1, r1)[2].astype(bool)
+    assert feas.sum() >= P // 2
+    rng = np.random.default_rng(7)
+    s2 = s1[feas].copy()
+    for k in range(s2.shape[0]):
+        idx = rng.choice(inst.E, size=int(rng.integers(1, 4)), replace=False)
+        s2[k, idx] = rng.integers(0, 45, size=idx.size)
+    r2 = o.assign_rooms(s2)
+    hot = _hot_events(inst, s2, r2)
+    assert (hot > 0).sum() >= s2.shape[0] // 2 and (4 * hot <= inst.E).all()   # the flagged path runs
+    seeds = ttga.population_seeds(2401, s2.shape[0])
+    for steps in (200, 1000):
+        s, r, g = dev(s2), dev(r2), dev(seeds)
+        dp.local_search(s, r, g, steps)
+        es, er, eg = o.local_search(s2, r2, seeds, steps)
+        assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg), steps
+        assert dp.status() == 0
+
+
 def test_rng_edge_seeds_vs_oracle(orc):
     """Park-Miller states outside [0, 2^31 - 1) take the 64-bit Schrage path on
     their first draw (Random.cc:27-37; every later state is in range and takes
