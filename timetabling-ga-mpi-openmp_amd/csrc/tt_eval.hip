@@ -444,6 +444,13 @@ constexpr int kT5Launches = 8, kT5MaxBlocks = 16384, kT5Words = 10;   // t0, id,
 __device__ unsigned long long g_t5_stamp[kT5Launches * kT5MaxBlocks * kT5Words];
 #endif
 
+// a.lo16 * b.hi16 + c in one VALU instruction (v_mad_u32_u16, op_sel on src1)
+__device__ __forceinline__ uint32_t mad_u16_hi(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[0,1,0,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 template <int EWC, int NW, int PK, bool DB = false>
 __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
                                                               const uint8_t* __restrict__ room, int P,
@@ -490,7 +497,9 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
         const int e = lane + 64 * r;
         const bool ok = e < E;
         if constexpr (PK == 1) {
-            inv_ps[r] = ok ? ((uint32_t)pb.poss[e] | ((uint32_t)pb.sn[e] << 16)) : 0xFFFFu;
+            // low half: the rooms NOT possible for e (one bfe gives the unsuitable-room
+            // term), high half: studentNumber (read by v_mad_u32_u16's op_sel)
+            inv_ps[r] = ok ? ((~(uint32_t)pb.poss[e] & 0xFFFFu) | ((uint32_t)pb.sn[e] << 16)) : 0u;
         } else {
             inv_poss[r] = ok ? (PossT)pb.poss[e] : (PossT)~0ull;
             inv_sn[r] = ok ? pb.sn[e] : 0;
@@ -608,9 +617,11 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
                         if (!(ablate & 8)) atomicOr((unsigned long long*)&B[s * EWC + r], 1ull << lane);
                         if (!(ablate & 16)) {                                   // Solution.cpp:148-150
 #if TT_T5_CELLS
-                            uint32_t* c = (uint32_t*)((uint8_t*)cnt + __umul24(s, (uint32_t)(4 * RW)) + ((ro >> 1) << 2));
+                            // dword s*RW + ro/2: byte offset 2*(s*2RW + (ro & ~1))
+                            uint32_t* c = (uint32_t*)((uint8_t*)cnt + ((__umul24(s, (uint32_t)(2 * RW)) + (ro & ~1u)) << 1));
                             const uint32_t sh = ro << 4;                        // shifts and bfe use bits 4:0
-                            h += (int)__builtin_amdgcn_ubfe(atomicAdd(c, 1u << (sh & 31u)), sh & 31u, 16);
+                            // (v_bfe_u32 reads offset bits 4:0, as the shift does)
+                            h += (int)__builtin_amdgcn_ubfe(atomicAdd(c, 1u << (sh & 31u)), sh, 16);
 #else
                             const uint32_t cell = s * (uint32_t)R + ro;
                             const uint32_t sh = (cell & 1u) << 4;
@@ -619,11 +630,11 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
                         }
                         const bool last_slot = (kLastSlotMask >> s) & 1ull;
                         if constexpr (PK == 1) {
-                            h += (int)(((inv_ps[r] >> ro) & 1u) ^ 1u);                  // :155-156
+                            h += (int)__builtin_amdgcn_ubfe(inv_ps[r], ro, 1);               // :155-156
 #if TT_T5_CELLS
-                            last += (int)((uint32_t)(kLastSlotMask >> s) & 1u) * (int)(inv_ps[r] >> 16);   // :93-96
+                            last = (int)mad_u16_hi((uint32_t)(kLastSlotMask >> s) & 1u, inv_ps[r], (uint32_t)last);   // :93-96
 #else
-                            last += last_slot ? (int)(inv_ps[r] >> 16) : 0;             // :93-96
+                            last += last_slot ? (int)(inv_ps[r] >> 16) : 0;             // :93-96 (unused: PK 1 with TT_T5_CELLS)
 #endif
                         } else {
                             h += (int)(((inv_poss[r] >> ro) & 1u) ^ 1u);

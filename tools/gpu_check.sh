@@ -92,6 +92,7 @@ for s in $STEPS; do
     gahot) for i in 1 2; do run ga8k_hot0_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot0.so; run ga8k_hot1_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot1.so; run ga8k_hot2_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_hot2.so; done ;;
     abocc) run ab_occ_med 300 python -u tools/ab_eval.py med 65536 t5old:8 t5old:7 occ:8 occ:7 && run ab_occ_lg 300 python -u tools/ab_eval.py lg 65536 t5old:8 t5old:7 occ:8 occ:7 && run ab_occ_comp01 300 python -u tools/ab_eval.py comp01 65536 t5old:8 occ:8 occ:7 ;;
     abeval) run ab_eval 300 python -u tools/ab_eval.py old new ;;
+    abt5) run ab_t5_med 300 python -u tools/ab_eval.py med 65536 old:8 new:8 old:7 new:7 && run ab_t5_lg 300 python -u tools/ab_eval.py lg 65536 old:8 new:8 && run ab_t5_comp01 300 python -u tools/ab_eval.py comp01 65536 old:8 new:8 && run ab_t5_med2 300 python -u tools/ab_eval.py med 65536 new:8 old:8 ;;
     abcorr) run ab_corr_syn 400 python -u tools/ab_eval.py syn 262144 old:13 new:13 && run ab_corr_med 300 python -u tools/ab_eval.py med 65536 old:8 new:8 ;;
     valurate) run valu_rate 120 tools/valu_rate ;;
     abls4) run ab4_comp01 400 python -u tools/ab_ls.py comp01 8192 old new noscv norow && run ab4_med 400 python -u tools/ab_ls.py med 4096 old new noscv norow ;;
