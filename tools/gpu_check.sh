@@ -65,6 +65,9 @@ for s in $STEPS; do
     ls1000) run bench_ls1000 300 python -u tools/bench_ls.py --pop 4096 --steps 1000 --pre-steps 3000 --cpu-sample 256 ;;
     ga8k)  run ga8k 400 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 512 ;;
     ga32k) run ga32k 300 python -u tools/bench_ga.py --config comp01 --pop 65536 --children 32768 --gens 10 --min-seconds 1.0 --steps 1000 --warm-gens 30 --warm-feasible 0.6 --cpu-sample 0 ;;
+    gacomps) for c in comp05 comp10 comp15 comp20; do run ga8k_$c 400 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 512; done ;;
+    abgate) run abgate_med 400 python -u tools/ab_ls.py med 4096 g1 g2 g3 g4 && run abgate_comp01 400 python -u tools/ab_ls.py comp01 8192 g1 g2 g3 g4 &&
+            for c in comp15 comp10 comp01; do for l in g1 g2 g3 g4; do run gagate_${c}_$l 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done ;;
     gatrace) run ga8k_trace 400 rocprofv3 --kernel-trace --stats -d "$OUT/ga_trace" -o run --output-format csv -- python -u tools/bench_ga.py $GA8K --gens 20 --cpu-sample 0 ;;
     lsprof) prof_fresh; run lsprof_ga 300 python -u tools/ls_prof.py --config comp01 --pop 65536 --children 8192 --from-ga 0.999 --steps 1000 ;;
     timeprob) run time_problem 600 python -u tools/time_problem.py "$OUT/time_problem.json" 5 ;;
