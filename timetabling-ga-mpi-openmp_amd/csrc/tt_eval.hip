@@ -650,8 +650,16 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
                     // not the ds_read2_b64 pairs the compiler forms (8 cycles per 1 KiB, 32 banks)
                     corr_words<0, EWC>(lds_addr(B), sv, inv_cup, lane, E, last_partial, h);   // :151-153
                 }
-                h = wave_sum(h);
-                last = wave_sum(last);
+                // one reduction of h << 16 | last when every lane's two parts are < 1024
+                // (so both 64-lane sums stay below 2^16), else two
+                if (!wave_any(h >= 1024 || last >= 1024)) {
+                    const uint32_t t = (uint32_t)wave_sum((h << 16) | last);
+                    h = (int)(t >> 16);
+                    last = (int)(t & 0xFFFFu);
+                } else {
+                    h = wave_sum(h);
+                    last = wave_sum(last);
+                }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
