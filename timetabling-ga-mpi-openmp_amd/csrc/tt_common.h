@@ -92,13 +92,29 @@ __device__ __forceinline__ int pm_pick(int64_t& s, int n) { return (int)__dmul_r
 // trips. Written out rather than __reduce_add_sync, whose library reduction
 // also carries a partial-EXEC path at every call site (code size: the local
 // search inlines it dozens of times).
+#ifndef TT_WAVE_SUM_BCAST
+#define TT_WAVE_SUM_BCAST 1
+#endif
 __device__ __forceinline__ int wave_sum(int v) {
+#if TT_WAVE_SUM_BCAST
+    // row_shr 1/2/4/8 leave row r's sum in lane 16r + 15; row_bcast:15 adds row r's
+    // into row r+1 (rows 1, 3), row_bcast:31 lane 31's into rows 2-3: lane 63 holds
+    // the wave's sum -- one readlane instead of four plus three scalar adds
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);    // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);    // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);    // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);    // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 (rows 1, 3)
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 (rows 2, 3)
+    return __builtin_amdgcn_readlane(v, 63);
+#else
     v += __builtin_amdgcn_update_dpp(0, v, 0x101, 0xf, 0xf, true);    // row_shl:1 (lane i += lane i+1)
     v += __builtin_amdgcn_update_dpp(0, v, 0x102, 0xf, 0xf, true);    // row_shl:2
     v += __builtin_amdgcn_update_dpp(0, v, 0x104, 0xf, 0xf, true);    // row_shl:4
     v += __builtin_amdgcn_update_dpp(0, v, 0x108, 0xf, 0xf, true);    // row_shl:8: lane 16r holds row r's sum
     return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
            __builtin_amdgcn_readlane(v, 48);
+#endif
 }
 
 // Wave ballot / any of a bool: the builtin takes the compare's lane mask as
