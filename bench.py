@@ -157,6 +157,10 @@ def main():
     # let a one-GPU box rehearse the N > 1 path (RCCL needs distinct GPUs)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     backend = os.environ.get("TTGA_BENCH_BACKEND", "nccl")
+    if backend == "nccl" and world > max(1, torch.cuda.device_count()):
+        # more ranks than GPUs: RCCL refuses two ranks on one device ("Duplicate GPU
+        # detected"), so the rehearsal takes gloo (the line says so in config.rehearsal)
+        backend = "gloo"
     use_dist = world > 1 or os.environ.get("TTGA_BENCH_FORCE_DIST", "") not in ("", "0")
     if use_dist and world == 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
