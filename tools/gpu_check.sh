@@ -68,6 +68,8 @@ for s in $STEPS; do
     gacomps) for c in comp05 comp10 comp15 comp20; do run ga8k_$c 400 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 512; done ;;
     abgate) run abgate_med 400 python -u tools/ab_ls.py med 4096 g1 g2 g3 g4 && run abgate_comp01 400 python -u tools/ab_ls.py comp01 8192 g1 g2 g3 g4 &&
             for c in comp15 comp10 comp01; do for l in g1 g2 g3 g4; do run gagate_${c}_$l 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done ;;
+    gasteady) run ga8k_steady_trace 500 rocprofv3 --kernel-trace -d "$OUT/ga_steady" -o run --output-format csv -- python -u tools/bench_ga.py --config comp01 --pop 65536 --children 8192 --steps 1000 --warm-gens 400 --warm-feasible 0.999 --gens 20 --cpu-sample 0 &&
+              python tools/trace_window.py "$OUT/ga_steady/run_kernel_trace.csv" 20 > "$OUT/ga_steady_window.json"; cat "$OUT/ga_steady_window.json" ;;
     gatrace) run ga8k_trace 400 rocprofv3 --kernel-trace --stats -d "$OUT/ga_trace" -o run --output-format csv -- python -u tools/bench_ga.py $GA8K --gens 20 --cpu-sample 0 ;;
     lsprof) prof_fresh; run lsprof_ga 300 python -u tools/ls_prof.py --config comp01 --pop 65536 --children 8192 --from-ga 0.999 --steps 1000 ;;
     timeprob) run time_problem 600 python -u tools/time_problem.py "$OUT/time_problem.json" 5 ;;
