@@ -66,9 +66,6 @@ ap.add_argument("--warm-feasible", type=float, default=1.1, help="stop warming o
 ap.add_argument("--lpt", choices=["auto", "on", "off"], default="auto",
                 help="longest-expected-first dispatch of the children's local search (Island default: auto)")
 ap.add_argument("--lib", default=None, help="profiling: an A/B build (tools/ab_build.sh) instead of the in-tree library")
-ap.add_argument("--graph", action="store_true",
-                help="replay one captured generation (a HIP graph: breed, LPT eval and order, local search + "
-                     "redo, eval, replace) instead of launching its kernels one by one")
 a = ap.parse_args()
 if a.lib:
     native._lib = native.load(pathlib.Path(a.lib).resolve())
@@ -88,21 +85,6 @@ warm = 1
 while warm < a.warm_gens and float(isl.pop["feasible"].float().mean().item()) < a.warm_feasible:
     isl.step()
     warm += 1
-graph = None
-if a.graph:
-    # one more warm generation on the capture stream (its per-stream local-search
-    # redo list is allocated outside the capture), then capture a generation
-    gs = torch.cuda.Stream()
-    gs.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(gs):
-        isl.step()
-    torch.cuda.current_stream().wait_stream(gs)
-    torch.cuda.synchronize()
-    warm += 1
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph, stream=gs):
-        isl.step()                          # recorded, not run
-    isl.generation -= 1
 feas_start = float(isl.pop["feasible"].float().mean().item())
 torch.cuda.synchronize()
 # snapshot of the population and child streams the CPU sample (and its device replay) breed from
@@ -113,11 +95,7 @@ snap_rng = isl.rng_child.clone()
 t0 = time.perf_counter()
 gens = 0
 while gens < a.gens or time.perf_counter() - t0 < a.min_seconds:
-    if graph is not None:
-        graph.replay()
-        isl.generation += 1
-    else:
-        isl.step()
+    isl.step()
     gens += 1
     # the generations are stream-ordered and need no host round trip; the clock is
     # checked against the device every 8 generations (a sync after every one left
@@ -138,7 +116,7 @@ out = {"config": a.config, "E": inst.E, "R": inst.R, "F": inst.F, "S": inst.S, "
        "children_per_gen": a.children, "gens": gens, "max_steps": a.steps, "lpt_dispatch": isl.lpt,
        "init_seconds": init_s,
        "warm_gens": warm, "feasible_fraction_at_start": feas_start,
-       "graph": bool(a.graph), "pop_digest": pop_digest, "gpu_seconds": gpu_s, "gpu_children_per_s": a.children * gens / gpu_s,
+       "pop_digest": pop_digest, "gpu_seconds": gpu_s, "gpu_children_per_s": a.children * gens / gpu_s,
        "best_scv_feasible": int(isl.pop["scv"][pf].min().item()) if bool(pf.any()) else None,
        "best": {"feasible": feas, "scv": scv, "hcv": hcv, "penalty": pen},
        "feasible_fraction": float(isl.pop["feasible"].float().mean().item())}
