@@ -4,7 +4,17 @@ individuals on the 400-event medium01-size instance, per GPU (weak scaling:
 one independent population shard per rank, no data-path collective).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config med|lg|syn|sm]
+    python bench.py --gpus N --config syn --global-pop 262144      (strong scaling)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+`--gpus N > 1` without a launcher (no WORLD_SIZE in the environment) starts its
+own N ranks: the parent, before it makes any GPU call, runs
+`python -m torch.distributed.run --nproc-per-node N ... bench.py` as a child
+process (the `mpiexec -n k` fan-out of ga.cpp:370-381), relays rank 0's JSON
+line and exits with the children's return code. N above the visible GPUs fails
+(rc 2) unless TTGA_BENCH_BACKEND=gloo asks for a rehearsal on fewer GPUs.
+`--global-pop G` splits G individuals across the ranks (strong scaling, BASELINE
+configs[4]); by default every rank evaluates --pop individuals (weak scaling).
 
 TTGA_BENCH_FORCE_DIST=1 initialises the process group (RCCL) at world 1 too, so
 the timing barrier and the MAX all-reduce run through RCCL on a one-GPU box
@@ -50,7 +60,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--warm-seconds", type=float, default=0.25,
                     help="keep warming up until this much wall time of launches has run")
-    ap.add_argument("--pop", type=int, default=POP_PER_GPU)
+    ap.add_argument("--pop", type=int, default=POP_PER_GPU, help="individuals per GPU (weak scaling)")
+    ap.add_argument("--global-pop", type=int, default=0,
+                    help="individuals over all ranks, split across them (strong scaling); overrides --pop")
     ap.add_argument("--config", default="med", choices=["sm", "med", "lg", "syn"])
     ap.add_argument("--variant", type=int, default=0, help="tt_eval kernel: 0 auto, 2 block, 7/8 tile5, 13 wide path")
     ap.add_argument("--cpu-sample", type=int, default=0,
@@ -59,7 +71,10 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 counter passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.global_pop and args.global_pop < max(1, args.gpus):
+        ap.error("--global-pop must be at least --gpus")
+    return args
 
 
 def _free_port() -> int:
@@ -127,16 +142,61 @@ def cpu_baseline(inst, slot_np, room_np, gpu_out):
 DOMINANT = {8: "eval_tile5_kernel", 13: "eval_", 2: "eval_block_kernel"}   # kernel name substrings
 
 
+def visible_gpus() -> int:
+    """GPUs this process may use, counted without initialising the GPU
+    (torch.cuda.device_count() does not, on this image)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(args) -> int:
+    """--gpus N > 1 with no launcher around us: run N ranks as child processes
+    of torch.distributed.run (one rank per GPU, 127.0.0.1 rendezvous) and relay
+    rank 0's JSON line. This process never touches the GPU."""
+    n = args.gpus
+    gpus = visible_gpus()
+    rehearsal = os.environ.get("TTGA_BENCH_BACKEND", "nccl") == "gloo"
+    if n > gpus and not rehearsal:
+        print(f"bench.py: --gpus {n} but {gpus} GPU(s) visible; set TTGA_BENCH_BACKEND=gloo to rehearse "
+              f"{n} ranks on fewer GPUs", file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(REPO / "bench.py"), *sys.argv[1:]]
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.Popen(cmd, cwd=str(REPO), env=env, stdout=subprocess.PIPE, text=True)
+    for ln in proc.stdout:                   # rank 0's line on stdout; anything else to stderr
+        (sys.stdout if ln.startswith("{") else sys.stderr).write(ln)
+        sys.stdout.flush()
+    return proc.wait()
+
+
+def rank_share(args, rank: int, world: int):
+    """(individuals of this rank, index of its first individual in the global
+    population, global population)."""
+    if args.global_pop > 0:
+        base, extra = divmod(args.global_pop, world)
+        p = base + (1 if rank < extra else 0)
+        start = rank * base + min(rank, extra)
+        return p, start, args.global_pop
+    return args.pop, rank * args.pop, args.pop * world
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.pmc_child:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    P, first, global_pop = rank_share(args, rank, world)
     pmc = None
     if world == 1 and not args.no_pmc and not args.pmc_child:
         # live counters of the same workload, before this process initialises the GPU
         sys.path.insert(0, str(REPO / "tools"))
         import pmc_live
         v = args.variant or (8 if args.config != "syn" else 13)
-        child = [str(REPO / "bench.py"), "--pmc-child", "--config", args.config, "--pop", str(args.pop),
+        child = [str(REPO / "bench.py"), "--pmc-child", "--config", args.config, "--pop", str(P),
                  "--steps", "20", "--warmup", "2", "--variant", str(v)]
         # FETCH_SIZE read-factor calibration: the same kernel with its evaluation phases
         # off (tile5: lane and wave phase; wide path: eval_lanes only), which reads
@@ -145,14 +205,13 @@ def main():
         calib[-1] = str(v | (0x30 if v in (7, 8) else 0x40 if v == 13 else 0))
         E = {"sm": 100, "syn": 2000}.get(args.config, 400)
         pmc = pmc_live.derive(pmc_live.collect(child, DOMINANT.get(v, "eval_"), calib if v in (7, 8, 13) else None),
-                              calib_bytes=float(args.pop) * E)
+                              calib_bytes=float(P) * E)
     import torch
     import torch.distributed as dist
 
     import ttga
     from ttga import native
 
-    rank = int(os.environ.get("RANK", "0"))
     # one rank per GPU; LOCAL_RANK modulo the visible GPUs and TTGA_BENCH_BACKEND=gloo
     # let a one-GPU box rehearse the N > 1 path (RCCL needs distinct GPUs)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
@@ -178,10 +237,10 @@ def main():
 
     inst = ttga.config_instance(args.config)
     dp = native.DeviceProblem(inst, device=local)
-    P, E = args.pop, inst.E
+    E = inst.E
     # synthetic population: RandomInitialSolution per individual (seed base 12345 + global index),
     # canonical rooms from the matcher; setup, not timed
-    seeds = torch.from_numpy(ttga.population_seeds(12345 + rank * P, P)).to(dev)
+    seeds = torch.from_numpy(ttga.population_seeds(12345 + first, P)).to(dev)
     slot = torch.empty((P, E), dtype=torch.uint8, device=dev)
     room = torch.empty_like(slot)
     dp.random_init(seeds, slot, room)
@@ -223,18 +282,23 @@ def main():
     if args.pmc_child:
         return
     if rank == 0:
-        total = P * world * args.steps
+        total = global_pop * args.steps
         value = total / wall_max
+        strong = args.global_pop > 0
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count    # CUs (256 on a whole MI355X)
         bytes_per_eval = 2 * E + 13                     # u8 slot+room in; i32 hcv,scv,penalty + u8 feasible out
         achieved = bytes_per_eval * P / (kernel_ms * 1e-3) / 1e9
         variant = args.variant or dp.eval_variant()
         line = {
             "metric": METRIC, "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "warmup_launches": launched, "ms_per_step": wall_max / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "i32", "data": "synthetic",
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "i32", "data": "synthetic",
             "config": {"workload": f"{args.config} instance E={E} R={inst.R} F={inst.F} S={inst.S} (seeded synthetic, "
-                                   f"{SIZE_NAMES[args.config]}), population {P} per GPU, one tt_eval (hcv+scv+feasible+penalty) "
-                                   f"per step", "pop_per_gpu": P, "global_pop": P * world,
+                                   f"{SIZE_NAMES[args.config]}), "
+                                   + (f"global population {global_pop} split over {world} GPU(s)" if strong
+                                      else f"population {P} per GPU")
+                                   + ", one tt_eval (hcv+scv+feasible+penalty) per step",
+                       "pop_per_gpu": P, "global_pop": global_pop,
                        "kernel": KERNELS[variant],
                        "parallelism": f"dp{world} (independent population shards)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -264,12 +328,12 @@ def main():
                 clk = pmc["cycles"] / (kernel_ms * 1e-3)
                 units = {"lds": {"cycles_per_individual": raw["SQ_LDS_IDX_ACTIVE"] / P,
                                  "frac": pmc.get("lds_busy"), "bank_conflict_share": pmc.get("lds_conflict"),
-                                 "only_us": raw["SQ_LDS_IDX_ACTIVE"] / (256 * clk) * 1e6,
+                                 "only_us": raw["SQ_LDS_IDX_ACTIVE"] / (ncu * clk) * 1e6,
                                  "peak": "1 LDS-array cycle per CU per shader cycle (MI355X_MICROARCH.md §LDS)"}}
                 if "SQ_INSTS_VALU" in raw:
                     units["valu"] = {"instructions_per_individual": raw["SQ_INSTS_VALU"] / P,
                                      "frac": pmc.get("valu_busy"),
-                                     "only_us": raw["SQ_INSTS_VALU"] / (256 * clk) * 1e6,
+                                     "only_us": raw["SQ_INSTS_VALU"] / (ncu * clk) * 1e6,
                                      "peak": "1 wave64 VALU instruction per CU per shader cycle (4 SIMDs x 4 cycles; "
                                              "tools/valu_rate, profiles/r04_j_valu_rate.json)"}
                 bind = max(units, key=lambda k: units[k]["frac"] or 0.0)
@@ -296,8 +360,8 @@ def main():
             rate = P * lookups / (lanes_ms * 1e-3)
             line["roofline"]["lane_phase"] = {
                 "kernel": "eval_lanes_w16", "kernel_ms": lanes_ms, "lookups_per_individual": lookups,
-                "lookups_per_s": rate, "peak_lookups_per_s": 32 * 256 * clk,
-                "frac": rate / (32 * 256 * clk), "clock_ghz": clk / 1e9,
+                "lookups_per_s": rate, "peak_lookups_per_s": 32 * ncu * clk,
+                "frac": rate / (32 * ncu * clk), "clock_ghz": clk / 1e9,
                 "peak_note": "ds_read_u8: 64 lanes in 2 LDS cycles (32 banks) per CU; clock from the live pass"}
         if world == 1 and not args.no_cpu:
             n = args.cpu_sample

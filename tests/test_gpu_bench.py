@@ -38,10 +38,17 @@ def test_bench_single_gpu_line():
     assert cb["matches_gpu"] is True and cb["value"] > 0 and cb["cores"] >= 1
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def test_bench_two_ranks_rehearsal():
     env = dict(os.environ, TTGA_BENCH_BACKEND="gloo")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29547", "bench.py", "--gpus", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
                         "--steps", "10", "--warmup", "2", "--no-pmc", "--no-cpu"],
                        cwd=REPO, capture_output=True, text=True, timeout=280, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -60,3 +67,28 @@ def test_bench_rccl_process_group_one_gpu():
     assert r.returncode == 0, r.stderr[-2000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == 1 and d["value"] > 0 and d["config"]["process_group"].startswith("nccl")
+
+
+def test_bench_self_launch_two_ranks():
+    """`bench.py --gpus 2` with no launcher: the parent starts the two ranks
+    itself (gloo rehearsal on a one-GPU box) and relays rank 0's line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["TTGA_BENCH_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "10", "--warmup", "2",
+                        "--no-pmc", "--no-cpu"], cwd=REPO, capture_output=True, text=True, timeout=280, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["global_pop"] == 131072 and d["scaling"] == "weak" and d["value"] > 0
+
+
+def test_bench_self_launch_global_pop_strong():
+    """--global-pop splits one population across the ranks (BASELINE configs[4])."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["TTGA_BENCH_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--global-pop", "65536", "--steps", "10",
+                        "--warmup", "2", "--no-pmc", "--no-cpu"], cwd=REPO, capture_output=True, text=True,
+                       timeout=280, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["global_pop"] == 65536 and d["config"]["pop_per_gpu"] == 32768

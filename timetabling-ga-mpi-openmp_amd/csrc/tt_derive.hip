@@ -161,6 +161,15 @@ int derive_on_device(const tt_problem* p, const uint32_t* atb, const int32_t* ro
     hipStream_t st = nullptr;
     TT_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     hipError_t he = hipMalloc(&tmp, total);
+    if (he == hipErrorOutOfMemory) {
+        // the transient attendance bit image (Ep x Sp / 8 bytes) does not fit: a size
+        // limit of this instance, not a device failure
+        (void)hipGetLastError();
+        (void)hipStreamDestroy(st);
+        set_error("tt_problem_create: the " + std::to_string(total >> 20) +
+                  " MiB derivation image (E x S attendance bits) does not fit in device memory");
+        return TT_ERR_LIMIT;
+    }
     if (he != hipSuccess) { (void)hipStreamDestroy(st); return check_hip(he, "derive: hipMalloc"); }
     uint32_t* dAt = (uint32_t*)tmp;
     int32_t* drs = (int32_t*)(tmp + at_bytes);

@@ -191,16 +191,18 @@ __device__ __forceinline__ void corr_words(uint32_t bbase, const uint32_t* sv, c
 }
 
 // ---------------------------------------------------------------- scalar record loads
-typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
-// 16 dwords through the scalar cache, issued now, waited for by sld_wait
-// (the compiler does not track this load: every use goes through sld_wait,
-// whose "+s" makes the registers depend on the wait).
-__device__ __forceinline__ u32x16 sload16(const uint32_t* p) {
-    u32x16 v;
-    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
-    return v;
+// Records come through the scalar cache by the compiler's own s_load (uniform
+// index into the constant address space), so it tracks every load and places
+// the s_waitcnt itself. (Round 4 issued them from inline asm with a separate
+// wait; the compiler could copy the destination registers between issue and
+// wait -- a data race that showed up once as nondeterministic wide-path
+// results. tests/test_native.py::test_no_untracked_scalar_loads checks the
+// built code object for asm-issued scalar loads.)
+template <int ST>
+__device__ __forceinline__ void sload_rec(const ConstU32* q, uint32_t (&r)[ST]) {
+#pragma unroll
+    for (int j = 0; j < ST; ++j) r[j] = q[j];
 }
-__device__ __forceinline__ void sld_wait(u32x16& v) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v) : : "memory"); }
 
 // ---------------------------------------------------------------- student runs
 // The lane phase over the size-sorted student lists (DevProblem::sid/srun):
@@ -253,7 +255,7 @@ template <bool GAP>
 __device__ __forceinline__ int mask_terms(uint64_t m) { return GAP ? mask_scv_gap(m) : mask_scv(m); }
 // K students of N ids whose dwords are r[0 .. K*N/2)
 template <int N, int K, bool GAP = false>
-__device__ __forceinline__ int students_scv(const uint8_t* my, const u32x16& r) {
+__device__ __forceinline__ int students_scv(const uint8_t* my, const uint32_t* r) {
     constexpr int H = N / 2;
     uint32_t sl[K * N];
 #pragma unroll
@@ -270,9 +272,9 @@ __device__ __forceinline__ int students_scv(const uint8_t* my, const u32x16& r) 
     }
     return sc;
 }
-// A run of cnt students of N ids from dword p: one 64-B scalar load per step
-// (two students when N <= 16), the next step's load issued before this step's
-// LDS reads (ping-pong registers).
+// A run of cnt students of N ids from dword p: one scalar load of K*N/2
+// dwords per step (K = 2 students when N <= 16), the next step's load issued
+// before this step's LDS reads (ping-pong registers, no copies).
 template <int N, int KMAX, bool GAP = false>
 __device__ __forceinline__ int run_scv(const uint8_t* my, const uint32_t* p, int cnt) {
     constexpr int K = N <= 16 ? KMAX : 1;
@@ -303,24 +305,24 @@ __device__ __forceinline__ int run_scv(const uint8_t* my, const uint32_t* p, int
         }
         return sc;
     }
+    const ConstU32* q = (const ConstU32*)p;
     if (steps > 0) {
         int i = 0;
-        u32x16 ra = sload16(p), rb;
+        uint32_t ra[ST], rb[ST];
+        sload_rec<ST>(q, ra);
         while (true) {
-            sld_wait(ra);
-            rb = sload16(p + (i + 1 < steps ? i + 1 : i) * ST);
+            sload_rec<ST>(q + (i + 1 < steps ? i + 1 : i) * ST, rb);
             sc += students_scv<N, K, GAP>(my, ra);
-            if (++i == steps) { sld_wait(rb); break; }
-            sld_wait(rb);
-            ra = sload16(p + (i + 1 < steps ? i + 1 : i) * ST);
+            if (++i == steps) break;
+            sload_rec<ST>(q + (i + 1 < steps ? i + 1 : i) * ST, ra);
             sc += students_scv<N, K, GAP>(my, rb);
-            if (++i == steps) { sld_wait(ra); break; }
+            if (++i == steps) break;
         }
     }
     if constexpr (K == 2) {
         if (cnt & 1) {
-            u32x16 r = sload16(p + steps * ST);
-            sld_wait(r);
+            uint32_t r[N / 2];
+            sload_rec<N / 2>(q + steps * ST, r);
             sc += students_scv<N, 1, GAP>(my, r);
         }
     }
@@ -1288,7 +1290,10 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
             std::atomic<int>& c = const_cast<tt_problem*>(p)->t5_occ[NW == 8][two];
             int per_cu = c.load(std::memory_order_relaxed);
             if (per_cu >= 0) return per_cu;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, bytes) != hipSuccess) return 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, bytes) != hipSuccess) {
+                (void)hipGetLastError();    // not sticky: the launch's own error check must not see it
+                return 0;
+            }
             c.store(per_cu, std::memory_order_relaxed);
             return per_cu;
         };

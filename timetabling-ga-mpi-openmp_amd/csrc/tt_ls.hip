@@ -482,6 +482,12 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
 #ifndef TT_LS_ROWPF
 #define TT_LS_ROWPF 0
 #endif
+// With the phase-1 eventHcv flags a skip moves the visit index by several
+// positions, so a row prefetched for position i+1 would belong to the wrong
+// event: the two are exclusive.
+#if TT_LS_ROWPF && (!defined(TT_LS_HOT) || TT_LS_HOT)
+#error "TT_LS_ROWPF needs TT_LS_HOT=0 (a flag skip invalidates the prefetched row)"
+#endif
 #ifndef TT_LS_SERIAL_CALL
 #define TT_LS_SERIAL_CALL 1
 #endif
@@ -1675,8 +1681,10 @@ static int ls_mask_occupancy(const tt_problem* p, int cap, K k) {
     const size_t b0 = ls_layout(p->E, p->R, p->dev.EW64, cap, 0).bytes, b1 = ls_layout(p->E, p->R, p->dev.EW64, cap, S).bytes;
     int o0 = 0, o1 = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o0, k, 64, b0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, k, 64, b1) != hipSuccess || o1 < 1)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, k, 64, b1) != hipSuccess || o1 < 1) {
+        (void)hipGetLastError();
         return 0;
+    }
     return (std::min(o0, 255) << 8) | std::min(o1, 255);
 }
 
@@ -1753,8 +1761,10 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
     TT_HIP(hipGetLastError());
     // the redo launch: resident waves only (an empty list costs one short launch)
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, local_search_redo_kernel, 64, Lf.bytes) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, local_search_redo_kernel, 64, Lf.bytes) != hipSuccess) {
+        (void)hipGetLastError();        // clear it: the redo launch's check below must see only its own error
         per_cu = 1;
+    }
     const int grid = std::min(P, std::max(1, per_cu) * p->num_cus);
     hipLaunchKernelGGL(local_search_redo_kernel, dim3(grid), dim3(64), Lf.bytes, st, p->dev, slot, room, rng,
                        max_steps, p1, p2, p3, rl->list, rl->cap, smf);

@@ -31,6 +31,7 @@ ap.add_argument("--from-ga", type=float, default=0.0,
                 help="profile the localSearch of GA children: an island (pop --pop, --children) is run until "
                      "this fraction of it is feasible, then one generation's bred children are searched")
 ap.add_argument("--children", type=int, default=32768)
+ap.add_argument("--warm-gens", type=int, default=400, help="--from-ga: at most this many generations first")
 a = ap.parse_args()
 
 lib = native.load(native.PKG_DIR / "libttga_prof.so")
@@ -47,7 +48,7 @@ if a.from_ga > 0:
     isl = Island(dp, pop_size=P, children=a.children, max_steps=a.steps, seed=42)
     isl.initialize()
     gens = 0
-    while float(isl.pop["feasible"].float().mean().item()) < a.from_ga and gens < 400:
+    while float(isl.pop["feasible"].float().mean().item()) < a.from_ga and gens < a.warm_gens:
         isl.step()
         gens += 1
     c = isl.child
@@ -66,7 +67,9 @@ torch.cuda.synchronize()
 n = lib.tt_ls_prof_read(buf, 1)
 v = {NAMES[i]: int(buf[i]) for i in range(n)}
 trials, waves = max(v["trials"], 1), max(v["waves"], 1)
-out = {"config": a.config, "pop": P, "max_steps": a.steps, "from_ga": a.from_ga, "raw": v,
+out = {"config": a.config, "pop": P, "max_steps": a.steps, "from_ga": a.from_ga,
+       "ga_generations": gens if a.from_ga > 0 else 0,
+       "feasible_at_start": float(isl.pop["feasible"].float().mean().item()) if a.from_ga > 0 else None, "raw": v,
        "cycles_per_trial": {k: v[k] / trials for k in NAMES[:7]},
        "cycles_per_wave": {k: v[k] / waves for k in NAMES[:8] + ["scramble", "visit_setup_p1", "move1_loop_p1",
                                                                   "move2_loop_p1", "phase1", "phase2", "visit_setup_p2",
