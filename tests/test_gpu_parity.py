@@ -14,7 +14,7 @@ from ttga import native  # noqa: E402
 
 NAMES = ["sm", "med", "tight"]
 # tt_eval kernels: 2 eval_block, 7/8 eval_tile5 (4/8 waves), 13 wide path (eval_lanes<16> + eval_corr)
-EVAL_VARIANTS = [2, 7, 8, 13]
+EVAL_VARIANTS = [2, 7, 8, 9, 13]
 
 
 def load(golden_dir, name):
@@ -157,6 +157,7 @@ def test_eval_bench_size_properties(orc):
     assert np.array_equal(orc.problem(inst).assign_rooms(s_np), r_np)
     for x, e in zip(a, exp):
         assert np.array_equal(x[idx], e)
+    assert dp.status() == 0          # eval_tile6's bounded queue wait (bit 5) never fired
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -259,6 +260,28 @@ def test_local_search_random_vs_oracle(orc):
     dp.local_search(s, r, g, 3000)
     es, er, eg = o.local_search(es, er, eg, 3000)
     assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg)
+
+
+@pytest.mark.parametrize("name", ["tight", "med"])
+def test_local_search_noncanonical_rooms_vs_oracle(orc, problems, name):
+    """The phase-1 room-pair bounds (TT_LS_P1B) use a slot's rooms as a maximum
+    matching only after checking that no augmenting path exists: localSearch
+    from random slots with rooms that assignRooms would not give (random, and
+    all room 0), on the tight instance (27 events without a possible room) and
+    med, against the oracle."""
+    dp, inst, z = problems[name]
+    o = orc.problem(inst)
+    P = 32
+    slots, _ = ttga.random_slots(ttga.population_seeds(3131, P), inst.E)
+    rng = np.random.default_rng(9)
+    rooms = rng.integers(0, inst.R, size=(P, inst.E), dtype=np.uint8)
+    rooms[::2] = 0
+    seeds = ttga.population_seeds(3232, P)
+    s, r, g = dev(slots), dev(rooms), dev(seeds)
+    dp.local_search(s, r, g, 300)
+    es, er, eg = o.local_search(slots, rooms, seeds, 300)
+    assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg)
+    assert dp.status() == 0
 
 
 def test_local_search_med_population_vs_oracle(orc):

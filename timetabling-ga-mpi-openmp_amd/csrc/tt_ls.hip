@@ -34,7 +34,7 @@ constexpr int kLsCapSmall = 64;
 // Profiling build (-DTT_LS_PROF, `make libttga_prof.so`, tools/ls_prof.py):
 // per-section shader-clock totals of every wave, summed into g_ls_prof.
 #ifdef TT_LS_PROF
-enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfQ1, kPfQ1c, kPfQ1m, kPfQ2, kPfQ2c, kPfQ2m, kPfP1m2, kPfP1m2lb, kPfP1m1m, kPfP1m1a, kPfP1m1k, kPfVis1, kPfM1p1, kPfM2p1, kPfPh1, kPfPh2, kPfVis2, kPfM1p2, kPfM2p2, kPfSkip1, kPfHot1, kPfMaxTotal, kPfN };
+enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfQ1, kPfQ1c, kPfQ1m, kPfQ2, kPfQ2c, kPfQ2m, kPfP1m2, kPfP1m2lb, kPfP1m1m, kPfP1m1a, kPfP1m1k, kPfVis1, kPfM1p1, kPfM2p1, kPfPh1, kPfPh2, kPfVis2, kPfM1p2, kPfM2p2, kPfSkip1, kPfHot1, kPfMaxTotal, kPfB1, kPfB2, kPfBInit, kPfN };
 __device__ unsigned long long g_ls_prof[kPfN];
 #define LSP_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define LSP_ADD(St, i, v) ((St).prof[i] += __builtin_amdgcn_s_memtime() - (v))
@@ -57,7 +57,7 @@ __device__ unsigned long long g_ls_prof[kPfN];
 #endif
 
 struct LsLayout {
-    size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, cnt, task, slp, pos, ps, sm;
+    size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, cnt, task, slp, pos, ps, sm, own;
     size_t task_bytes;
     int NT;              // events per matcher task (min(E, 256))
     size_t bytes;
@@ -85,6 +85,13 @@ struct LsLayout {
 #define TT_LS_SMASK 1
 #endif
 constexpr size_t kSmaskMaxBytes = 4096;
+// TT_LS_P1B: phase-1 room-pair lower bounds (below, pairs_lb) from an owner
+// table own[slot][room] of a maximum matching of every slot, kept for R <= 16
+// (45 * R u16 per wave).
+#ifndef TT_LS_P1B
+#define TT_LS_P1B 1
+#endif
+constexpr int kP1bMaxRooms = 16;
 // cap: events per matcher task (kLsCapSmall for the first launch, kMaxSlotEvents for the redo launch)
 // S: students with phase-2 masks (0: none)
 __host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap, int S) {
@@ -116,6 +123,7 @@ __host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap, int
     L.NB = b; b += 8 * (size_t)kLsTasks * EW;
     L.rp = b; b += 4 * (size_t)kSlots;
     L.hist = b; b += 2 * (size_t)kSlots * R;
+    L.own = b; if (TT_LS_P1B && R <= kP1bMaxRooms) b += 2 * (size_t)kSlots * R;   // phase-1 owner table
     al(4); L.misc = b; b += 4 * 32;
     L.cnt = b; b += 4 * (size_t)kMaxRooms;
     L.NT = E < cap ? E : cap;
@@ -165,6 +173,12 @@ struct LsState {
     // phase 2: the state stays feasible, so every slot's rooms are distinct and
     // hist[] is reused as the owner table oe[slot * R + room] (event, 0xFFFF free)
     int phase2;
+    // phase-1 pair bounds (TT_LS_P1B): own[t * R + r] = the event matched to room r
+    // in a maximum matching of slot t (0xFFFF: free), valid for the slots in trust;
+    // npw (lane w) = word w of the events without a possible room. Null own: off.
+    uint16_t* own;
+    uint64_t trust;
+    uint64_t npw;
 #ifdef TT_LS_PROF
     uint64_t prof[kPfN];
 #endif
@@ -700,6 +714,7 @@ __device__ __forceinline__ void cache_drop(LsState& S) {
     }
 }
 
+__device__ __forceinline__ void own_rebuild(LsState& S, int t);
 __device__ __forceinline__ void accept(LsState& S) {
     LSP_T(t0);
     S.c1_valid = 0;
@@ -755,6 +770,14 @@ __device__ __forceinline__ void accept(LsState& S) {
             }
     }
     wave_sync();
+    if (S.own) {                      // phase-1 pair bounds: the re-matched slots' owners (reference rooms)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (k >= S.nts) break;
+            own_rebuild(S, S.ts[k]);
+            S.trust |= 1ull << S.ts[k];
+        }
+    }
     LSP_ADD(S, kPfSync, t0);
 }
 
@@ -910,6 +933,138 @@ __device__ __forceinline__ bool matchable(LsState& S, int s, int out, int a) {
     return false;
 }
 
+// ---- phase-1 room-pair lower bounds (TT_LS_P1B). A phase-1 trial from an
+// infeasible state mostly fails on room clashes, which the correlation bounds
+// above cannot see, so it used to run the full matcher of every touched slot
+// just to be rejected. assignRooms (Solution.cpp:772-891) computes a MAXIMUM
+// matching, so an unmatched event has no free possible room and goes to its
+// first possible room, which is matched: each unmatched event with a possible
+// room adds at least one clash pair. Hence for a touched slot s' (the current
+// slot s, minus `out`, plus `a`):
+//     pairs(s') >= |s'| - M(s') - Z(s')
+// with Z the events without a possible room and M the maximum matching size;
+// M(s + a) = M(s) + [augmenting path from a] exactly, and M(s - out + a) <=
+// M(s + a) (a vertex removed never enlarges a matching). M(s) and the path
+// come from own[s], a maximum matching of every trusted slot: the matched
+// rooms of the current rooms (a room holding an event for which it is possible
+// has exactly one matched event; any such event will do), verified at the
+// start of phase 1 by an augmenting-path search from every unmatched event
+// (the caller's rooms need not come from assignRooms), and rebuilt from the
+// reference matcher's rooms whenever a slot is re-matched by an accepted move.
+// A trial whose correlation bound plus these pair bounds already reaches the
+// current value is rejected exactly as its full evaluation would reject it.
+// (Inlined: as out-of-line calls with plain arguments -- a reference to LsState
+// would put it in scratch -- the call sites' register saves doubled the
+// kernel's VGPR spills, 55 -> 112.)
+struct OwnArgs {
+    uint16_t* own;
+    const uint64_t* B;
+    const uint8_t* sl;
+    const uint8_t* rr;
+    const uint16_t* ps;
+    const uint64_t* poss;
+    int E, R, EW;
+};
+__device__ __forceinline__ OwnArgs own_args(const LsState& S) {
+    return OwnArgs{S.own, S.B, S.sl, S.rr, S.ps, S.pb.poss, S.E, S.R, S.EW};
+}
+__device__ __forceinline__ uint64_t own_poss(const OwnArgs& A, int e) { return A.ps ? (uint64_t)A.ps[e] : A.poss[e]; }
+
+__device__ __forceinline__ void own_rebuild_call(OwnArgs A, int t) {
+    const int lane = threadIdx.x & 63;
+    if (lane < A.R) A.own[t * A.R + lane] = 0xFFFF;
+    wave_sync();
+    for (int w = 0; w < A.EW; ++w) {
+        const int e = 64 * w + lane;
+        if ((A.B[(size_t)t * A.EW + w] >> lane) & 1ull) {
+            const int r = A.rr[e];
+            if ((own_poss(A, e) >> r) & 1ull) A.own[t * A.R + r] = (uint16_t)e;
+        }
+    }
+    wave_sync();
+}
+__device__ __forceinline__ void own_rebuild(LsState& S, int t) { own_rebuild_call(own_args(S), t); }
+
+// augmenting path from event a over own[s] (the room lanes' owners and their
+// possible rooms); M = the matching's size
+__device__ __forceinline__ bool own_aug(const OwnArgs& A, int s, int a, int& M) {
+    const int R = A.R, lane = threadIdx.x & 63;
+    const int o = lane < R ? (int)A.own[s * R + lane] : 0xFFFF;
+    const bool valid = o != 0xFFFF;
+    const uint64_t po = valid ? own_poss(A, o) : 0ull;
+    const uint64_t used = ballot(valid);
+    M = __popcll(used);
+    const uint64_t fre = (R >= 64 ? ~0ull : ((1ull << R) - 1)) & ~used;
+    uint64_t seen = own_poss(A, a);
+    if (seen & fre) return true;
+    uint64_t fr = seen & used;
+    while (fr) {
+        const int r = __builtin_ctzll(fr);
+        fr &= fr - 1;
+        const uint64_t nx = readlane64(po, r) & ~seen;
+        if (nx & fre) return true;
+        seen |= nx;
+        fr |= nx & used;
+    }
+    return false;
+}
+
+// lower bound on the clash pairs of slot s minus `out` (-1: none) plus event a
+// after the reference's re-match (s trusted)
+__device__ __forceinline__ int pairs_lb_call(OwnArgs A, uint64_t npw, int s, int out, int a) {
+    const int lane = threadIdx.x & 63;
+    int M;
+    const bool aug = own_aug(A, s, a, M);
+    const uint64_t bw = lane < A.EW ? A.B[(size_t)s * A.EW + lane] : 0ull;
+    const int nz = wave_sum((__popcll(bw) << 16) | __popcll(bw & npw));
+    const int N = (nz >> 16) + (out < 0 ? 1 : 0);
+    const int Z = (nz & 0xFFFF) + (own_poss(A, a) == 0ull) - (out >= 0 && own_poss(A, out) == 0ull);
+    const int u = N - M - (aug ? 1 : 0) - Z;
+    return u > 0 ? u : 0;
+}
+__device__ __forceinline__ int pairs_lb(LsState& S, int s, int out, int a) {
+    if (!((S.trust >> s) & 1ull)) return 0;
+    return pairs_lb_call(own_args(S), S.npw, s, out, a);
+}
+
+// start of phase 1: own[] for every slot from the current rooms and the
+// trusted slots (no augmenting path from any unmatched event)
+__device__ __forceinline__ uint64_t own_init_call(OwnArgs A) {
+    const int E = A.E, R = A.R, lane = threadIdx.x & 63;
+    for (int c = lane; c < kSlots * R; c += 64) A.own[c] = 0xFFFF;
+    wave_sync();
+    for (int e = lane; e < E; e += 64) {
+        const int t = A.sl[e], r = A.rr[e];
+        if ((own_poss(A, e) >> r) & 1ull) A.own[t * R + r] = (uint16_t)e;
+    }
+    wave_sync();
+    uint64_t trust = (1ull << kSlots) - 1ull;
+    for (int k = 0; 64 * k < E; ++k) {                          // wave-uniform
+        const int e = 64 * k + lane;
+        const bool unm = e < E && own_poss(A, e) != 0ull && A.own[A.sl[e] * R + A.rr[e]] != e;
+        for (uint64_t m = ballot(unm); m; m &= m - 1) {
+            const int eu = 64 * k + __builtin_ctzll(m);
+            const int t = A.sl[eu];
+            if (!((trust >> t) & 1ull)) continue;
+            int M;
+            if (own_aug(A, t, eu, M)) trust &= ~(1ull << t);      // not a maximum matching
+        }
+    }
+    return trust;
+}
+__device__ __forceinline__ void own_init(LsState& S) {
+    LSP_T(t0);
+    // lane w: word w of the events without a possible room
+    S.npw = 0;
+    for (int k = 0; 64 * k < S.E; ++k) {                        // wave-uniform
+        const int e = 64 * k + S.lane;
+        const uint64_t m = ballot(e < S.E && poss_of(S, e) == 0ull);
+        if (S.lane == k) S.npw = m;
+    }
+    S.trust = own_init_call(own_args(S));
+    LSP_ADD(S, kPfBInit, t0);
+}
+
 // ---- trial windows. A Move1/Move2 loop spends most of its trials on moves
 // the cheap tests above reject. Up to 64 consecutive trials are screened at
 // once, one per lane: lane k takes the trial k+1 draws ahead (Park-Miller jump:
@@ -1036,6 +1191,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     S.c1_valid = 0;
     S.listed = 0;
     S.phase2 = 0;
+    S.own = nullptr; S.trust = 0; S.npw = 0;
 #ifdef TT_LS_PROF
 #pragma unroll
     for (int i = 0; i < kPfN; ++i) S.prof[i] = 0;
@@ -1149,6 +1305,11 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
             nhot = wave_sum(lane < EW ? __popcll(hot) : 0);
         }
         const bool hotm = TT_LS_HOT && fast1 && 4 * nhot <= E;
+        // many events in conflict: room-pair lower bounds before the matcher (TT_LS_P1B)
+        if (TT_LS_P1B && !hotm && fast1 && R <= kP1bMaxRooms) {
+            S.own = (uint16_t*)(lds + L.own);
+            own_init(S);
+        }
         for (int i = 0; evc < E; i = wrap_e(i + 1, E)) {
             if (step > max_steps || ++guard > guard_max) break;
             if (hotm) {
@@ -1236,6 +1397,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         if (match_tasks(S, 2)) goto redo;
                         const int lb = (fast1 ? __builtin_amdgcn_readlane(V.x, t) : corr_nb(S, ei)) + S.misc[1];
                         if (lb >= c) { S.c1_valid = 1; continue; }
+                        if (S.own && lb + pairs_lb(S, t, -1, ei) >= c) { LSP_CNT(S, kPfB1); S.c1_valid = 1; continue; }
                         LSP_CNT(S, kPfP1m1m);
                         if (match_tasks(S, 1)) goto redo;
                         if (lb + S.misc[0] < c) { LSP_CNT(S, kPfP1m1a); accept(S);
@@ -1313,6 +1475,11 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         const int lb = corr_nb(S, ei) + corr_nb(S, ej);    // n >= lb whatever the rooms
                         LSP_CNT(S, kPfP1m2);
                         if (lb >= c) break;
+                        if (S.own && S.nts == 2 &&
+                            lb + pairs_lb(S, S.ts[0], ej, ei) + pairs_lb(S, S.ts[1], ei, ej) >= c) {
+                            LSP_CNT(S, kPfB2);
+                            break;
+                        }
                         LSP_CNT(S, kPfP1m2lb);
                         const TaskRegs tr = load_tasks(S, 7);
                         if (S.nts == 2) {             // task 0 = slot(ej) plus ei, task 1 = slot(ei) plus ej
@@ -1371,6 +1538,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     if (feasible_now(S)) {                                              // phase 2 (Solution.cpp:619-768)
         // owner table in place of the room histogram (rooms are distinct per slot now)
         S.phase2 = 1;
+        S.own = nullptr;
         for (int c = lane; c < kSlots * R; c += 64) S.hist[c] = 0xFFFF;
         if (TT_LS_SMASK && smS > 0) {
             S.sm = (uint64_t*)(lds + L.sm);
@@ -1577,7 +1745,8 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     LSP_CNT(S, kPfWaves);
     if (lane == 0) {
 #pragma unroll
-        for (int i = 0; i < kPfMaxTotal; ++i) atomicAdd(&g_ls_prof[i], (unsigned long long)S.prof[i]);
+        for (int i = 0; i < kPfN; ++i)
+            if (i != kPfMaxTotal) atomicAdd(&g_ls_prof[i], (unsigned long long)S.prof[i]);
         atomicMax(&g_ls_prof[kPfMaxTotal], (unsigned long long)S.prof[kPfTotal]);   // the slowest wave
     }
 #endif

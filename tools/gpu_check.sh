@@ -106,6 +106,12 @@ for s in $STEPS; do
     abr5) run ab_r5_syn 400 python -u tools/ab_eval.py syn 262144 r4:13 r5a:13 r4:13 r5a:13 && run ab_r5_med 300 python -u tools/ab_eval.py med 65536 r4:8 r5a:8 ;;
     lsprofc) prof_fresh; for c in comp15 comp10; do run lsprof_ga_$c 400 python -u tools/ls_prof.py --config $c --pop 65536 --children 8192 --from-ga 0.6 --warm-gens 96 --steps 1000; done ;;
     pmcgac) PMC_LAST=10 pmc pmc_ga_comp15 local_search_kernel python -u tools/bench_ga.py --config comp15 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 10 --cpu-sample 0 ;;
+    abr5b) run ab_r5b_syn 400 python -u tools/ab_eval.py syn 262144 r4:13 r5b:13 r4:13 r5b:13 &&
+           run ab_r5b_med 300 python -u tools/ab_eval.py med 65536 r4:8 r5b:8 r5b:9 r4:8 r5b:9 &&
+           run ab_r5b_lg 300 python -u tools/ab_eval.py lg 65536 r4:8 r5b:9 r4:8 r5b:9 &&
+           run ab_r5b_comp01 300 python -u tools/ab_eval.py comp01 65536 r4:8 r5b:9 r4:8 r5b:9 ;;
+    gap1b) for c in comp15 comp10 comp01; do for l in r5b0 r5b; do run ga8k_${c}_$l 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done &&
+           run ga8k_comp15_check 300 python -u tools/bench_ga.py --config comp15 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 512 ;;
     selftest) run bench_self2 300 env TTGA_BENCH_BACKEND=gloo python -u bench.py --gpus 2 --steps 20 --warmup 2 --no-pmc --no-cpu ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python -u bench.py --no-pmc --no-cpu --steps 100 ;;
     *) echo "unknown step $s"; exit 2 ;;

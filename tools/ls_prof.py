@@ -20,7 +20,8 @@ NAMES = ["init", "build_and_match", "match_task_wave", "corr_in_set", "scv_terms
          "p2_move1", "p2_move1_corr_ok", "p2_move1_match_ok", "p2_move2", "p2_move2_corr_ok", "p2_move2_match_ok",
          "p1_move2_quick", "p1_move2_lb_ok", "p1_move1_matched", "p1_move1_accepted", "p1_move1_kept_task",
          "visit_setup_p1", "move1_loop_p1", "move2_loop_p1", "phase1", "phase2", "visit_setup_p2", "move1_loop_p2",
-         "move2_loop_p2", "skip_p1", "hot_flags_p1", "max_total"]
+         "move2_loop_p2", "skip_p1", "hot_flags_p1", "max_total", "p1_move1_bound_rejects",
+         "p1_move2_bound_rejects", "pair_bound_init"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="med")
@@ -74,7 +75,7 @@ out = {"config": a.config, "pop": P, "max_steps": a.steps, "from_ga": a.from_ga,
        "cycles_per_wave": {k: v[k] / waves for k in NAMES[:8] + ["scramble", "visit_setup_p1", "move1_loop_p1",
                                                                   "move2_loop_p1", "phase1", "phase2", "visit_setup_p2",
                                                                   "move1_loop_p2", "move2_loop_p2", "skip_p1",
-                                                                  "hot_flags_p1"]},
+                                                                  "hot_flags_p1", "pair_bound_init"]},
        "trials_per_wave": v["trials"] / waves, "visits_per_wave": v["event_visits"] / waves,
        "slowest_wave_cycles": v["max_total"], "slowest_over_mean": v["max_total"] / max(v["total"] / waves, 1),
        "note": "s_memtime deltas summed over waves that finished in the first launch; sections nest "
