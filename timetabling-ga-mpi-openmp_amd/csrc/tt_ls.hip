@@ -57,7 +57,7 @@ __device__ unsigned long long g_ls_prof[kPfN];
 #endif
 
 struct LsLayout {
-    size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, cnt, task, slp, pos, ps, sm, own;
+    size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, cnt, task, slp, pos, ps, sm, sinf;
     size_t task_bytes;
     int NT;              // events per matcher task (min(E, 256))
     size_t bytes;
@@ -85,13 +85,16 @@ struct LsLayout {
 #define TT_LS_SMASK 1
 #endif
 constexpr size_t kSmaskMaxBytes = 4096;
-// TT_LS_P1B: phase-1 room-pair lower bounds (below, pairs_lb) from an owner
-// table own[slot][room] of a maximum matching of every slot, kept for R <= 16
-// (45 * R u16 per wave).
+// TT_LS_P1B: phase-1 room-pair lower bounds (below, SlotInfo) from a summary
+// of a maximum matching of every slot (45 x 20 B per wave + 128 B scratch).
 #ifndef TT_LS_P1B
 #define TT_LS_P1B 1
 #endif
-constexpr int kP1bMaxRooms = 16;
+struct SlotInfo {
+    uint64_t used;       // rooms matched in a maximum matching of the slot
+    uint64_t fr;         // rooms from which an alternating path reaches a free room (free rooms included)
+};
+constexpr size_t kSinfBytes = (16 + 4) * kSlots + 128;   // SlotInfo[45], nz[45] (N << 16 | Z, bit 31 trusted), owners
 // cap: events per matcher task (kLsCapSmall for the first launch, kMaxSlotEvents for the redo launch)
 // S: students with phase-2 masks (0: none)
 __host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap, int S) {
@@ -123,7 +126,7 @@ __host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap, int
     L.NB = b; b += 8 * (size_t)kLsTasks * EW;
     L.rp = b; b += 4 * (size_t)kSlots;
     L.hist = b; b += 2 * (size_t)kSlots * R;
-    L.own = b; if (TT_LS_P1B && R <= kP1bMaxRooms) b += 2 * (size_t)kSlots * R;   // phase-1 owner table
+    al(8); L.sinf = b; if (TT_LS_P1B) b += kSinfBytes;                  // phase-1 slot summaries
     al(4); L.misc = b; b += 4 * 32;
     L.cnt = b; b += 4 * (size_t)kMaxRooms;
     L.NT = E < cap ? E : cap;
@@ -173,11 +176,11 @@ struct LsState {
     // phase 2: the state stays feasible, so every slot's rooms are distinct and
     // hist[] is reused as the owner table oe[slot * R + room] (event, 0xFFFF free)
     int phase2;
-    // phase-1 pair bounds (TT_LS_P1B): own[t * R + r] = the event matched to room r
-    // in a maximum matching of slot t (0xFFFF: free), valid for the slots in trust;
-    // npw (lane w) = word w of the events without a possible room. Null own: off.
-    uint16_t* own;
-    uint64_t trust;
+    // phase-1 pair bounds (TT_LS_P1B): per-slot matching summaries (sinf, nz) and
+    // npw (lane w) = word w of the events without a possible room. Null sinf: off.
+    SlotInfo* sinf;
+    int32_t* nz;         // [45] N << 16 | Z, bit 31: the summary is of a maximum matching
+    uint16_t* own;       // [64] scratch: the owner of each room while a summary is built
     uint64_t npw;
 #ifdef TT_LS_PROF
     uint64_t prof[kPfN];
@@ -714,7 +717,7 @@ __device__ __forceinline__ void cache_drop(LsState& S) {
     }
 }
 
-__device__ __forceinline__ void own_rebuild(LsState& S, int t);
+__device__ __forceinline__ void sinf_build(LsState& S, int t);
 __device__ __forceinline__ void accept(LsState& S) {
     LSP_T(t0);
     S.c1_valid = 0;
@@ -770,12 +773,11 @@ __device__ __forceinline__ void accept(LsState& S) {
             }
     }
     wave_sync();
-    if (S.own) {                      // phase-1 pair bounds: the re-matched slots' owners (reference rooms)
+    if (S.sinf) {                     // phase-1 pair bounds: the re-matched slots' summaries (reference rooms)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             if (k >= S.nts) break;
-            own_rebuild(S, S.ts[k]);
-            S.trust |= 1ull << S.ts[k];
+            sinf_build(S, S.ts[k]);
         }
     }
     LSP_ADD(S, kPfSync, t0);
@@ -944,124 +946,84 @@ __device__ __forceinline__ bool matchable(LsState& S, int s, int out, int a) {
 //     pairs(s') >= |s'| - M(s') - Z(s')
 // with Z the events without a possible room and M the maximum matching size;
 // M(s + a) = M(s) + [augmenting path from a] exactly, and M(s - out + a) <=
-// M(s + a) (a vertex removed never enlarges a matching). M(s) and the path
-// come from own[s], a maximum matching of every trusted slot: the matched
-// rooms of the current rooms (a room holding an event for which it is possible
-// has exactly one matched event; any such event will do), verified at the
-// start of phase 1 by an augmenting-path search from every unmatched event
-// (the caller's rooms need not come from assignRooms), and rebuilt from the
-// reference matcher's rooms whenever a slot is re-matched by an accepted move.
-// A trial whose correlation bound plus these pair bounds already reaches the
-// current value is rejected exactly as its full evaluation would reject it.
-// (Inlined: as out-of-line calls with plain arguments -- a reference to LsState
-// would put it in scratch -- the call sites' register saves doubled the
-// kernel's VGPR spills, 55 -> 112.)
-struct OwnArgs {
-    uint16_t* own;
-    const uint64_t* B;
-    const uint8_t* sl;
-    const uint8_t* rr;
-    const uint16_t* ps;
-    const uint64_t* poss;
-    int E, R, EW;
-};
-__device__ __forceinline__ OwnArgs own_args(const LsState& S) {
-    return OwnArgs{S.own, S.B, S.sl, S.rr, S.ps, S.pb.poss, S.E, S.R, S.EW};
-}
-__device__ __forceinline__ uint64_t own_poss(const OwnArgs& A, int e) { return A.ps ? (uint64_t)A.ps[e] : A.poss[e]; }
-
-__device__ __forceinline__ void own_rebuild_call(OwnArgs A, int t) {
-    const int lane = threadIdx.x & 63;
-    if (lane < A.R) A.own[t * A.R + lane] = 0xFFFF;
+// M(s + a) (a vertex removed never enlarges a matching). Per slot the kernel
+// keeps a summary of one maximum matching: its matched rooms `used` and the
+// rooms `fr` from which an alternating path (room -> its matched event -> a
+// possible room of that event -> ...) reaches a free room, free rooms
+// included. An augmenting path from a new event a exists iff poss(a) meets fr,
+// so the bound costs a few bit operations per touched slot -- cheap enough
+// for every lane of a trial window. The matching is read off the current
+// rooms (a room holding an event for which it is possible has exactly one
+// matched event; any such event will do) and checked: it is maximum iff no
+// unmatched event has a possible room in fr (Berge); a slot that fails
+// (rooms the caller chose, not assignRooms) is untrusted and gets no bound
+// until an accepted move re-matches it with the reference matcher. A trial
+// whose correlation bound plus these pair bounds already reaches the current
+// value is rejected exactly as its full evaluation would reject it.
+__device__ __forceinline__ void sinf_build(LsState& S, int t) {
+    const int R = S.R, EW = S.EW, lane = S.lane;
+    if (lane < R) S.own[lane] = 0xFFFF;
     wave_sync();
-    for (int w = 0; w < A.EW; ++w) {
+    for (int w = 0; w < EW; ++w) {
         const int e = 64 * w + lane;
-        if ((A.B[(size_t)t * A.EW + w] >> lane) & 1ull) {
-            const int r = A.rr[e];
-            if ((own_poss(A, e) >> r) & 1ull) A.own[t * A.R + r] = (uint16_t)e;
+        if ((S.B[(size_t)t * EW + w] >> lane) & 1ull) {
+            const int r = S.rr[e];
+            if ((poss_of(S, e) >> r) & 1ull) S.own[r] = (uint16_t)e;
         }
     }
     wave_sync();
-}
-__device__ __forceinline__ void own_rebuild(LsState& S, int t) { own_rebuild_call(own_args(S), t); }
-
-// augmenting path from event a over own[s] (the room lanes' owners and their
-// possible rooms); M = the matching's size
-__device__ __forceinline__ bool own_aug(const OwnArgs& A, int s, int a, int& M) {
-    const int R = A.R, lane = threadIdx.x & 63;
-    const int o = lane < R ? (int)A.own[s * R + lane] : 0xFFFF;
+    const int o = lane < R ? (int)S.own[lane] : 0xFFFF;
     const bool valid = o != 0xFFFF;
-    const uint64_t po = valid ? own_poss(A, o) : 0ull;
+    const uint64_t po = valid ? poss_of(S, o) : 0ull;
     const uint64_t used = ballot(valid);
-    M = __popcll(used);
-    const uint64_t fre = (R >= 64 ? ~0ull : ((1ull << R) - 1)) & ~used;
-    uint64_t seen = own_poss(A, a);
-    if (seen & fre) return true;
-    uint64_t fr = seen & used;
-    while (fr) {
-        const int r = __builtin_ctzll(fr);
-        fr &= fr - 1;
-        const uint64_t nx = readlane64(po, r) & ~seen;
-        if (nx & fre) return true;
-        seen |= nx;
-        fr |= nx & used;
+    uint64_t fr = (R >= 64 ? ~0ull : ((1ull << R) - 1)) & ~used;
+    for (;;) {                                            // least fixed point, <= R rounds
+        const uint64_t fn = fr | ballot(valid && (po & fr) != 0ull);
+        if (fn == fr) break;
+        fr = fn;
     }
-    return false;
+    // N, Z and the maximality check (an unmatched event with a possible room in fr)
+    int n = 0, z = 0;
+    bool aug = false;
+    for (int w = 0; w < EW; ++w) {
+        const uint64_t bw = S.B[(size_t)t * EW + w];
+        n += __popcll(bw);
+        z += __popcll(bw & readlane64(S.npw, w));
+        const int e = 64 * w + lane;
+        if ((bw >> lane) & 1ull) aug |= S.own[S.rr[e]] != e && (poss_of(S, e) & fr) != 0ull;
+    }
+    const bool trusted = !wave_any(aug);
+    if (lane == 0) {
+        S.sinf[t].used = used;
+        S.sinf[t].fr = fr;
+        S.nz[t] = (trusted ? (int)0x80000000 : 0) | (n << 16) | z;
+    }
+    wave_sync();
 }
 
 // lower bound on the clash pairs of slot s minus `out` (-1: none) plus event a
-// after the reference's re-match (s trusted)
-__device__ __forceinline__ int pairs_lb_call(OwnArgs A, uint64_t npw, int s, int out, int a) {
-    const int lane = threadIdx.x & 63;
-    int M;
-    const bool aug = own_aug(A, s, a, M);
-    const uint64_t bw = lane < A.EW ? A.B[(size_t)s * A.EW + lane] : 0ull;
-    const int nz = wave_sum((__popcll(bw) << 16) | __popcll(bw & npw));
-    const int N = (nz >> 16) + (out < 0 ? 1 : 0);
-    const int Z = (nz & 0xFFFF) + (own_poss(A, a) == 0ull) - (out >= 0 && own_poss(A, out) == 0ull);
-    const int u = N - M - (aug ? 1 : 0) - Z;
+// after the reference's re-match (0 for an untrusted slot); any lanes
+__device__ __forceinline__ int pairs_lb_of(const SlotInfo& I, int nz, uint64_t pa, uint64_t pout, bool has_out) {
+    if (nz >= 0) return 0;                                     // bit 31 clear: untrusted
+    const int N = ((nz >> 16) & 0x7FFF) + (has_out ? 0 : 1);
+    const int Z = (nz & 0xFFFF) + (pa == 0ull) - (has_out && pout == 0ull);
+    const int u = N - __popcll(I.used) - ((pa & I.fr) != 0ull) - Z;
     return u > 0 ? u : 0;
 }
 __device__ __forceinline__ int pairs_lb(LsState& S, int s, int out, int a) {
-    if (!((S.trust >> s) & 1ull)) return 0;
-    return pairs_lb_call(own_args(S), S.npw, s, out, a);
+    return pairs_lb_of(S.sinf[s], S.nz[s], poss_of(S, a), out >= 0 ? poss_of(S, out) : 0ull, out >= 0);
 }
 
-// start of phase 1: own[] for every slot from the current rooms and the
-// trusted slots (no augmenting path from any unmatched event)
-__device__ __forceinline__ uint64_t own_init_call(OwnArgs A) {
-    const int E = A.E, R = A.R, lane = threadIdx.x & 63;
-    for (int c = lane; c < kSlots * R; c += 64) A.own[c] = 0xFFFF;
-    wave_sync();
-    for (int e = lane; e < E; e += 64) {
-        const int t = A.sl[e], r = A.rr[e];
-        if ((own_poss(A, e) >> r) & 1ull) A.own[t * R + r] = (uint16_t)e;
-    }
-    wave_sync();
-    uint64_t trust = (1ull << kSlots) - 1ull;
-    for (int k = 0; 64 * k < E; ++k) {                          // wave-uniform
-        const int e = 64 * k + lane;
-        const bool unm = e < E && own_poss(A, e) != 0ull && A.own[A.sl[e] * R + A.rr[e]] != e;
-        for (uint64_t m = ballot(unm); m; m &= m - 1) {
-            const int eu = 64 * k + __builtin_ctzll(m);
-            const int t = A.sl[eu];
-            if (!((trust >> t) & 1ull)) continue;
-            int M;
-            if (own_aug(A, t, eu, M)) trust &= ~(1ull << t);      // not a maximum matching
-        }
-    }
-    return trust;
-}
-__device__ __forceinline__ void own_init(LsState& S) {
+// start of phase 1: the no-room event words and every slot's summary
+__device__ __forceinline__ void sinf_init(LsState& S) {
     LSP_T(t0);
-    // lane w: word w of the events without a possible room
     S.npw = 0;
     for (int k = 0; 64 * k < S.E; ++k) {                        // wave-uniform
         const int e = 64 * k + S.lane;
         const uint64_t m = ballot(e < S.E && poss_of(S, e) == 0ull);
         if (S.lane == k) S.npw = m;
     }
-    S.trust = own_init_call(own_args(S));
+    for (int t = 0; t < kSlots; ++t) sinf_build(S, t);
     LSP_ADD(S, kPfBInit, t0);
 }
 
@@ -1191,7 +1153,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     S.c1_valid = 0;
     S.listed = 0;
     S.phase2 = 0;
-    S.own = nullptr; S.trust = 0; S.npw = 0;
+    S.sinf = nullptr; S.nz = nullptr; S.own = nullptr; S.npw = 0;
 #ifdef TT_LS_PROF
 #pragma unroll
     for (int i = 0; i < kPfN; ++i) S.prof[i] = 0;
@@ -1306,9 +1268,11 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
         }
         const bool hotm = TT_LS_HOT && fast1 && 4 * nhot <= E;
         // many events in conflict: room-pair lower bounds before the matcher (TT_LS_P1B)
-        if (TT_LS_P1B && !hotm && fast1 && R <= kP1bMaxRooms) {
-            S.own = (uint16_t*)(lds + L.own);
-            own_init(S);
+        if (TT_LS_P1B && !hotm && fast1) {
+            S.sinf = (SlotInfo*)(lds + L.sinf);
+            S.nz = (int32_t*)(S.sinf + kSlots);
+            S.own = (uint16_t*)(S.nz + kSlots);
+            sinf_init(S);
         }
         for (int i = 0; evc < E; i = wrap_e(i + 1, E)) {
             if (step > max_steps || ++guard > guard_max) break;
@@ -1357,6 +1321,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
             // accepted, and every acceptance leaves this event's loops
             const int eah_i = fast1 ? S.rp[t_orig] + __builtin_amdgcn_readlane(V.x, t_orig) - (int)row_bit(V.row, ei)
                                     : eah_cur(S, ei);
+            const uint64_t pei = S.sinf ? poss_of(S, ei) : 0ull;        // for the pair bounds
             LSP_ADD(S, kPfVis1, t_vis);
             LSP_T(t_m1);
             const int t_start = pm_pick(st, kSlots);
@@ -1369,7 +1334,9 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                     const int rem = kSlots - h;
                     const int tk = (t_start + h + lane) % kSlots;
                     const int xt = bperm(V.x, tk);                          // every lane takes part
-                    const bool skip = tk != t_orig && xt + S.misc[1] >= eah_i + S.rp[tk];
+                    // with the pair bound of slot tk plus ei (TT_LS_P1B) when the summaries are kept
+                    const int ub = S.sinf ? pairs_lb_of(S.sinf[tk], S.nz[tk], pei, 0ull, false) : 0;
+                    const bool skip = tk != t_orig && xt + S.misc[1] + ub >= eah_i + S.rp[tk];
                     const bool need = lane < rem && !skip;
                     bool done;
                     const int ks = window_resolve(lane, jump, st, step, max_steps, rem, p1, need, done);
@@ -1397,7 +1364,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         if (match_tasks(S, 2)) goto redo;
                         const int lb = (fast1 ? __builtin_amdgcn_readlane(V.x, t) : corr_nb(S, ei)) + S.misc[1];
                         if (lb >= c) { S.c1_valid = 1; continue; }
-                        if (S.own && lb + pairs_lb(S, t, -1, ei) >= c) { LSP_CNT(S, kPfB1); S.c1_valid = 1; continue; }
+                        if (S.sinf && lb + pairs_lb(S, t, -1, ei) >= c) { LSP_CNT(S, kPfB1); S.c1_valid = 1; continue; }
                         LSP_CNT(S, kPfP1m1m);
                         if (match_tasks(S, 1)) goto redo;
                         if (lb + S.misc[0] < c) { LSP_CNT(S, kPfP1m1a); accept(S);
@@ -1450,7 +1417,12 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                                 if (w == (ei >> 6)) cij = (int)((rw >> (ei & 63)) & 1ull);
                             }
                             const int c = eah_i + S.rp[tj] + c1 - selfj;
-                            const int lb = xt - cij + c2;
+                            int lb = xt - cij + c2;
+                            if (S.sinf) {                          // pair bounds of both touched slots
+                                const uint64_t pej = poss_of(S, ej);
+                                lb += pairs_lb_of(S.sinf[tj], S.nz[tj], pei, pej, true) +
+                                      pairs_lb_of(S.sinf[t_orig], S.nz[t_orig], pej, pei, true);
+                            }
                             need = lb < c;
                         }
                         bool done;
@@ -1475,7 +1447,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                         const int lb = corr_nb(S, ei) + corr_nb(S, ej);    // n >= lb whatever the rooms
                         LSP_CNT(S, kPfP1m2);
                         if (lb >= c) break;
-                        if (S.own && S.nts == 2 &&
+                        if (S.sinf && S.nts == 2 &&
                             lb + pairs_lb(S, S.ts[0], ej, ei) + pairs_lb(S, S.ts[1], ei, ej) >= c) {
                             LSP_CNT(S, kPfB2);
                             break;
@@ -1538,7 +1510,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     if (feasible_now(S)) {                                              // phase 2 (Solution.cpp:619-768)
         // owner table in place of the room histogram (rooms are distinct per slot now)
         S.phase2 = 1;
-        S.own = nullptr;
+        S.sinf = nullptr;
         for (int c = lane; c < kSlots * R; c += 64) S.hist[c] = 0xFFFF;
         if (TT_LS_SMASK && smS > 0) {
             S.sm = (uint64_t*)(lds + L.sm);
