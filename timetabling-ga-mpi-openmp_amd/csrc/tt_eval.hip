@@ -464,6 +464,14 @@ __device__ __forceinline__ uint32_t mad_u16_hi(uint32_t a, uint32_t b, uint32_t 
     return d;
 }
 
+// TT_T5_PRIO: issue priority falls as a wave gets through its tile (3 in the
+// lane phase, 2 for its first half of individuals, 1 after), so of a CU's two
+// resident workgroups the one further behind wins the arbiter -- instead of
+// the older one (round-4 stamps: the older finishes 31.9 us, its neighbour
+// 43.0 us, and the CU's last workgroup runs alone for 15 us).
+#ifndef TT_T5_PRIO
+#define TT_T5_PRIO 0
+#endif
 template <int EWC, int NW, int PK, bool DB = false>
 __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
                                                               const uint8_t* __restrict__ room, int P,
@@ -574,7 +582,9 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
         // kept live across the tile loop, the product spilled to scratch)
         uint32_t lsp;
         asm volatile("v_mul_u32_u24 %0, %1, %2" : "=v"(lsp) : "v"(lane), "s"(SP));
+        if (TT_T5_PRIO) __builtin_amdgcn_s_setprio(3);
         const int sc = (!(ablate & 1) && r0 < r1) ? lane_scv_runs<1>(tile + lsp, pb, r0, r1) : 0;
+        if (TT_T5_PRIO) __builtin_amdgcn_s_setprio(2);
         part[wv * 64 + lane] = sc;
 
         // ---- wave phase (wave = individual): hcv terms + last-slot term
@@ -603,6 +613,7 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
 #endif
         if (wv < nq) load_row(room, wv, pfn);
         for (int q = wv; q < nq; q += NW) {
+            if (TT_T5_PRIO && q == wv + 4 * NW) __builtin_amdgcn_s_setprio(1);
             uint32_t rv[EWC], sv[EWC];
 #pragma unroll
             for (int r = 0; r < EWC; ++r) rv[r] = pfn[r];
@@ -739,6 +750,14 @@ __host__ __device__ inline Tile6Layout tile6_layout(int E, int R) {
 }
 constexpr int kT6WaitBound = 1 << 22;           // s_sleep rounds before status bit 5 (never reached)
 
+// tile rows by byte copies (E % 4 != 0: no dword LDS-DMA), rows w0, w0 + nw, ...;
+// out of line, so the copy loop's registers stay out of the kernel's item loop
+__device__ __noinline__ void t6_stage_bytes(const uint8_t* src, uint8_t* dst, int n, int E, int SP, int w0, int nw) {
+    const int lane = threadIdx.x & 63;
+    for (int r = w0; r < n; r += nw)
+        for (int c = lane; c < E; c += 64) dst[r * SP + c] = src[(long)r * E + c];
+}
+
 template <int EWC, int PK, int NCH>
 __global__ __launch_bounds__(64 * kT6Waves, 1) void eval_tile6_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
                                                                     const uint8_t* __restrict__ room, int P,
@@ -803,8 +822,7 @@ __global__ __launch_bounds__(64 * kT6Waves, 1) void eval_tile6_kernel(DevProblem
             if (nw == NW) tile_dma<NW>(src, dst, n, E, SP, w0, lane);
             else tile_dma<1>(src, dst, n, E, SP, 0, lane);
         } else {
-            for (int r = w0; r < n; r += nw)
-                for (int c = lane; c < E; c += 64) dst[r * SP + c] = src[(long)r * E + c];
+            t6_stage_bytes(src, dst, n, E, SP, w0, nw);
         }
     };
     for (int k = 0; k < 2 && k < my_tiles; ++k) stage(k, lds + k * L.tile_bytes, wv, NW);
@@ -832,6 +850,12 @@ __global__ __launch_bounds__(64 * kT6Waves, 1) void eval_tile6_kernel(DevProblem
         q = i >= NCH ? i - NCH : -1;
     };
 
+    // LDS ordering: the DS instructions of one wave execute in issue order and the
+    // tile DMA has landed (vmcnt) before its ready word is written, so the queue
+    // words need no release/acquire fences -- only compiler barriers. (An acq_rel
+    // atomic waits for vmcnt(0), i.e. for the next individual's room-row prefetch,
+    // at every item.)
+    int seen[2] = {0, 1};                                      // ready words last seen per buffer
     uint32_t pfn[EWC];
     int cur = grab();
     {
@@ -853,15 +877,17 @@ __global__ __launch_bounds__(64 * kT6Waves, 1) void eval_tile6_kernel(DevProblem
             if (nxt < total && q2 >= 0 && q2 < np_of(k2)) load_row(k2, q2, pfn);     // next individual's rooms
         }
         // this item's tile must be staged
-        if (__hip_atomic_load(&ctl[3 + b], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != k) {
+        if ((b ? seen[1] : seen[0]) != k) {
             int spins = 0;
-            while (__hip_atomic_load(&ctl[3 + b], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != k) {
+            while (__hip_atomic_load(&ctl[3 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != k) {
                 __builtin_amdgcn_s_sleep(2);
                 if (++spins > kT6WaitBound) {
                     if (lane == 0) atomicOr(pb.status, 32);
                     break;
                 }
             }
+            if (b) seen[1] = k; else seen[0] = k;
+            asm volatile("" ::: "memory");
         }
         const uint8_t* tile = lds + b * L.tile_bytes;
         const int np = np_of(k);
@@ -932,8 +958,10 @@ __global__ __launch_bounds__(64 * kT6Waves, 1) void eval_tile6_kernel(DevProblem
         }
         // ---- item done; the wave that completes the tile writes it out and stages tile k + 2
         int old = 0;
-        if (lane == 0) old = __hip_atomic_fetch_add(&ctl[1 + b], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("" ::: "memory");
+        if (lane == 0) old = __hip_atomic_fetch_add(&ctl[1 + b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         old = __builtin_amdgcn_readfirstlane(old);
+        asm volatile("" ::: "memory");
         if (old == NI - 1) {
             const int kn = k + 2;
             if (kn < my_tiles) stage(kn, lds + b * L.tile_bytes, 0, 1);
@@ -951,8 +979,8 @@ __global__ __launch_bounds__(64 * kT6Waves, 1) void eval_tile6_kernel(DevProblem
             }
             part[b * 64 + lane] = 0;
             if (lane == 0) ctl[1 + b] = 0;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         // the DMA has landed
-            if (lane == 0) __hip_atomic_store(&ctl[3 + b], kn, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // the DMA has landed, the resets are done
+            if (lane == 0) __hip_atomic_store(&ctl[3 + b], kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         cur = nxt;
     }

@@ -94,7 +94,8 @@ struct SlotInfo {
     uint64_t used;       // rooms matched in a maximum matching of the slot
     uint64_t fr;         // rooms from which an alternating path reaches a free room (free rooms included)
 };
-constexpr size_t kSinfBytes = (16 + 4) * kSlots + 128;   // SlotInfo[45], nz[45] (N << 16 | Z, bit 31 trusted), owners
+// SlotInfo[45], the matcher tasks' SlotInfo[3], nz[45] (N << 16 | Z, bit 31: trusted), the tasks' nz[3], owners[64]
+constexpr size_t kSinfBytes = 16 * (kSlots + 3) + 4 * (kSlots + 3) + 128;
 // cap: events per matcher task (kLsCapSmall for the first launch, kMaxSlotEvents for the redo launch)
 // S: students with phase-2 masks (0: none)
 __host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap, int S) {
@@ -181,6 +182,9 @@ struct LsState {
     SlotInfo* sinf;
     int32_t* nz;         // [45] N << 16 | Z, bit 31: the summary is of a maximum matching
     uint16_t* own;       // [64] scratch: the owner of each room while a summary is built
+    SlotInfo* tsi;       // [3] summaries of the matcher tasks' slots (the wave matcher's result)
+    int32_t* tnz;        // [3]
+    int tvalid;          // bit k: tsi[k] / tnz[k] describe the current neighbour's task k
     uint64_t npw;
 #ifdef TT_LS_PROF
     uint64_t prof[kPfN];
@@ -482,6 +486,25 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
     if (act) S.nrr[ev] = (uint8_t)r;
     if (lane < R) T.hist[lane] = (uint16_t)cnt_r;
     if (lane == 0) S.misc[k] = pr;
+    if (S.sinf) {
+        // phase-1 pair bounds: this maximum matching's summary (see SlotInfo), read off
+        // the registers -- room lane j: its matched event's possible rooms (plr)
+        const bool mj = (rmatched >> lane) & 1ull;
+        const uint64_t plr = ((uint64_t)plr_hi << 32) | plr_lo;
+        uint64_t fr = (R >= 64 ? ~0ull : ((1ull << R) - 1)) & ~rmatched;
+        for (;;) {
+            const uint64_t fn = fr | ballot(mj && (plr & fr) != 0ull);
+            if (fn == fr) break;
+            fr = fn;
+        }
+        const int z = __popcll(ballot(act && pl == 0ull));
+        if (lane == 0) {
+            S.tsi[k].used = rmatched;
+            S.tsi[k].fr = fr;
+            S.tnz[k] = (int)0x80000000 | (N << 16) | z;
+        }
+        S.tvalid |= 1 << k;
+    }
     LSP_ADD(S, kPfMatch, t0);
 }
 
@@ -646,6 +669,7 @@ __device__ __forceinline__ bool match_tasks(LsState& S, int kmask, const TaskReg
                 const LsTask T = get_task(S, k);
                 S.misc[k] = match_task_serial(S.R, N, S.pb.poss, T.ev, T.pl, T.mr, T.rm, T.dr, T.hist, S.nrr);
             }
+            S.tvalid &= ~(1 << k);                                  // accept rebuilds this slot's summary
             wave_sync();
         }
     }
@@ -777,8 +801,13 @@ __device__ __forceinline__ void accept(LsState& S) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             if (k >= S.nts) break;
-            sinf_build(S, S.ts[k]);
+            if ((S.tvalid >> k) & 1) {                     // from the wave matcher's own result
+                if (S.lane == 0) { S.sinf[S.ts[k]] = S.tsi[k]; S.nz[S.ts[k]] = S.tnz[k]; }
+            } else {
+                sinf_build(S, S.ts[k]);
+            }
         }
+        wave_sync();
     }
     LSP_ADD(S, kPfSync, t0);
 }
@@ -795,6 +824,7 @@ __device__ __forceinline__ void add_touched(LsState& S, int t) {
 __device__ __forceinline__ void set_move(LsState& S, int type, int e1, int a2, int e3) {
     // type 1: e1 -> slot a2; type 2: swap e1, a2; type 3: e1->slot(a2), a2->slot(e3), e3->slot(e1)
     S.nts = 0;
+    S.tvalid = S.c1_valid ? (S.tvalid & 2) : 0;             // a kept task 1 keeps its summary
     if (type == 1) {
         S.nmv = 1; S.mv_e[0] = e1; S.mv_t[0] = a2;
         add_touched(S, a2); add_touched(S, S.sl[e1]);
@@ -1014,16 +1044,66 @@ __device__ __forceinline__ int pairs_lb(LsState& S, int s, int out, int a) {
     return pairs_lb_of(S.sinf[s], S.nz[s], poss_of(S, a), out >= 0 ? poss_of(S, out) : 0ull, out >= 0);
 }
 
-// start of phase 1: the no-room event words and every slot's summary
+// start of phase 1: the no-room event words and every slot's summary, all
+// slots at once: owners of every (slot, room) in the matcher task scratch
+// (free at this point), then the used masks, the fr fixed point over all
+// slots together, and the maximality check (sinf_build slot by slot when
+// the 45 x R owner table does not fit the task scratch)
 __device__ __forceinline__ void sinf_init(LsState& S) {
     LSP_T(t0);
+    const int E = S.E, R = S.R, lane = S.lane;
     S.npw = 0;
-    for (int k = 0; 64 * k < S.E; ++k) {                        // wave-uniform
-        const int e = 64 * k + S.lane;
-        const uint64_t m = ballot(e < S.E && poss_of(S, e) == 0ull);
-        if (S.lane == k) S.npw = m;
+    for (int k = 0; 64 * k < E; ++k) {                          // wave-uniform
+        const int e = 64 * k + lane;
+        const uint64_t m = ballot(e < E && poss_of(S, e) == 0ull);
+        if (lane == k) S.npw = m;
     }
-    for (int t = 0; t < kSlots; ++t) sinf_build(S, t);
+    const int NC = kSlots * R;
+    if ((size_t)2 * NC > (size_t)kLsTasks * S.task_bytes) {
+        for (int t = 0; t < kSlots; ++t) sinf_build(S, t);
+        LSP_ADD(S, kPfBInit, t0);
+        return;
+    }
+    uint16_t* own2 = (uint16_t*)S.task_base;                    // [45][R]
+    const uint64_t rmask = R >= 64 ? ~0ull : ((1ull << R) - 1);
+    const uint32_t rinv = ((1u << 20) + (uint32_t)R - 1) / (uint32_t)R;   // c / R = (c * rinv) >> 20 for c < 2^12
+    for (int c = lane; c < NC; c += 64) own2[c] = 0xFFFF;
+    if (lane < kSlots) { S.sinf[lane].used = 0ull; S.nz[lane] = (int)0x80000000; }
+    wave_sync();
+    for (int e = lane; e < E; e += 64) {
+        const int t = S.sl[e], r = S.rr[e];
+        const uint64_t pe = poss_of(S, e);
+        if ((pe >> r) & 1ull) own2[t * R + r] = (uint16_t)e;
+        atomicAdd(&S.nz[t], (1 << 16) | (pe == 0ull ? 1 : 0));
+    }
+    wave_sync();
+    for (int c = lane; c < NC; c += 64) {
+        const int t = (int)(((uint32_t)c * rinv) >> 20), r = c - t * R;
+        if (own2[c] != 0xFFFF) atomicOr((unsigned long long*)&S.sinf[t].used, 1ull << r);
+    }
+    wave_sync();
+    if (lane < kSlots) S.sinf[lane].fr = rmask & ~S.sinf[lane].used;
+    wave_sync();
+    for (;;) {                                                  // fr of every slot, least fixed point
+        bool ch = false;
+        for (int c = lane; c < NC; c += 64) {
+            const int t = (int)(((uint32_t)c * rinv) >> 20), r = c - t * R;
+            const int o = own2[c];
+            const uint64_t f = S.sinf[t].fr;
+            if (o != 0xFFFF && !((f >> r) & 1ull) && (poss_of(S, o) & f) != 0ull) {
+                atomicOr((unsigned long long*)&S.sinf[t].fr, 1ull << r);
+                ch = true;
+            }
+        }
+        wave_sync();
+        if (!wave_any(ch)) break;
+    }
+    for (int e = lane; e < E; e += 64) {                        // Berge: no unmatched event reaches a free room
+        const int t = S.sl[e];
+        const uint64_t pe = poss_of(S, e);
+        if (pe != 0ull && own2[t * R + S.rr[e]] != e && (pe & S.sinf[t].fr) != 0ull) atomicAnd(&S.nz[t], 0x7FFFFFFF);
+    }
+    wave_sync();
     LSP_ADD(S, kPfBInit, t0);
 }
 
@@ -1154,6 +1234,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     S.listed = 0;
     S.phase2 = 0;
     S.sinf = nullptr; S.nz = nullptr; S.own = nullptr; S.npw = 0;
+    S.tsi = nullptr; S.tnz = nullptr; S.tvalid = 0;
 #ifdef TT_LS_PROF
 #pragma unroll
     for (int i = 0; i < kPfN; ++i) S.prof[i] = 0;
@@ -1270,8 +1351,10 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
         // many events in conflict: room-pair lower bounds before the matcher (TT_LS_P1B)
         if (TT_LS_P1B && !hotm && fast1) {
             S.sinf = (SlotInfo*)(lds + L.sinf);
-            S.nz = (int32_t*)(S.sinf + kSlots);
-            S.own = (uint16_t*)(S.nz + kSlots);
+            S.tsi = S.sinf + kSlots;
+            S.nz = (int32_t*)(S.tsi + 3);
+            S.tnz = S.nz + kSlots;
+            S.own = (uint16_t*)(S.tnz + 3);
             sinf_init(S);
         }
         for (int i = 0; evc < E; i = wrap_e(i + 1, E)) {

@@ -51,109 +51,121 @@ from ttga.ga import Island  # noqa: E402
 sys.path.insert(0, str(REPO))
 from bench import host_cores  # noqa: E402  (every core this job may use + the CPU model)
 
-ap = argparse.ArgumentParser()
-ap.add_argument("--config", default="comp01")
-ap.add_argument("--pop", type=int, default=65536)
-ap.add_argument("--children", type=int, default=65536)
-ap.add_argument("--gens", type=int, default=3)
-ap.add_argument("--min-seconds", type=float, default=0.0,
-                help="keep running timed generations until at least this much time has passed")
-ap.add_argument("--steps", type=int, default=200, help="maxSteps (-p 1: 200, -p 2: 1000, else 2000)")
-ap.add_argument("--seed", type=int, default=42)
-ap.add_argument("--cpu-sample", type=int, default=512)
-ap.add_argument("--warm-gens", type=int, default=0, help="at most this many untimed generations first")
-ap.add_argument("--warm-feasible", type=float, default=1.1, help="stop warming once this fraction is feasible")
-ap.add_argument("--lpt", choices=["auto", "on", "off"], default="auto",
-                help="longest-expected-first dispatch of the children's local search (Island default: auto)")
-ap.add_argument("--lib", default=None, help="profiling: an A/B build (tools/ab_build.sh) instead of the in-tree library")
-a = ap.parse_args()
-if a.lib:
-    native._lib = native.load(pathlib.Path(a.lib).resolve())
-
-inst = ttga.config_instance(a.config)
-dp = native.DeviceProblem(inst)
-isl = Island(dp, pop_size=a.pop, children=a.children, max_steps=a.steps, seed=a.seed,
-             lpt=None if a.lpt == "auto" else a.lpt == "on")
-torch.cuda.synchronize()
-t0 = time.perf_counter()
-isl.initialize()
-torch.cuda.synchronize()
-init_s = time.perf_counter() - t0
-isl.step()                                  # warm-up generation
-torch.cuda.synchronize()
-warm = 1
-while warm < a.warm_gens and float(isl.pop["feasible"].float().mean().item()) < a.warm_feasible:
-    isl.step()
-    warm += 1
-feas_start = float(isl.pop["feasible"].float().mean().item())
-torch.cuda.synchronize()
-# snapshot of the population and child streams the CPU sample (and its device replay) breed from
-pop_slot, pop_room = isl.pop["slot"].cpu().numpy().copy(), isl.pop["room"].cpu().numpy().copy()
-pop_pen = isl.pop["penalty"].cpu().numpy().copy()
-snap = {k: v.clone() for k, v in isl.pop.items()}
-snap_rng = isl.rng_child.clone()
-t0 = time.perf_counter()
-gens = 0
-while gens < a.gens or time.perf_counter() - t0 < a.min_seconds:
-    isl.step()
-    gens += 1
-    # the generations are stream-ordered and need no host round trip; the clock is
-    # checked against the device every 8 generations (a sync after every one left
-    # the GPU idle while the host enqueued the next generation's launches)
-    if gens >= a.gens and gens % 8 == 0:
-        torch.cuda.synchronize()
-torch.cuda.synchronize()
-gpu_s = time.perf_counter() - t0
-feas, scv, hcv, pen = isl.member_meta(0)
-# digest of the final population (slots, rooms, penalties): equal runs, equal digests
 import hashlib  # noqa: E402
-_h = hashlib.sha256()
-for _k in ("slot", "room", "penalty"):
-    _h.update(isl.pop[_k].cpu().numpy().tobytes())
-pop_digest = _h.hexdigest()[:16]
-pf = isl.pop["feasible"].bool()
-out = {"config": a.config, "E": inst.E, "R": inst.R, "F": inst.F, "S": inst.S, "pop": a.pop,
-       "children_per_gen": a.children, "gens": gens, "max_steps": a.steps, "lpt_dispatch": isl.lpt,
-       "init_seconds": init_s,
-       "warm_gens": warm, "feasible_fraction_at_start": feas_start,
-       "pop_digest": pop_digest, "gpu_seconds": gpu_s, "gpu_children_per_s": a.children * gens / gpu_s,
-       "best_scv_feasible": int(isl.pop["scv"][pf].min().item()) if bool(pf.any()) else None,
-       "best": {"feasible": feas, "scv": scv, "hcv": hcv, "penalty": pen},
-       "feasible_fraction": float(isl.pop["feasible"].float().mean().item())}
 
 from oracle_lib import ref  # noqa: E402
-R = ref()
-if R is not None and a.cpu_sample > 0:
-    n = min(a.cpu_sample, a.children)
-    threads, total, model = host_cores()
-    h = R.problem(inst)
-    seeds = snap_rng[:n].cpu().numpy().copy()
-    res = {}
-    for as_is in (1, 0):       # as_is = 0 last: its children are the ones compared
-        ref_children, ref_rng, res[as_is] = h.ga_children(pop_slot, pop_room, pop_pen, seeds, a.steps, threads, as_is)
-    # the device replay of the same children from the snapshot
-    c = {k: torch.empty_like(v[:n]) for k, v in snap.items()}
-    g = torch.from_numpy(seeds).cuda()
-    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    dp.ga_breed(snap["slot"], snap["room"], snap["penalty"], g, c["slot"], c["room"], fl, isl.p_cross, isl.p_mut, True)
-    dp.local_search(c["slot"], c["room"], g, a.steps)
-    dp.eval(c["slot"], c["room"], out=(c["hcv"], c["scv"], c["feasible"], c["penalty"]))
+
+
+def parser():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="comp01")
+    ap.add_argument("--pop", type=int, default=65536)
+    ap.add_argument("--children", type=int, default=65536)
+    ap.add_argument("--gens", type=int, default=3)
+    ap.add_argument("--min-seconds", type=float, default=0.0,
+                    help="keep running timed generations until at least this much time has passed")
+    ap.add_argument("--steps", type=int, default=200, help="maxSteps (-p 1: 200, -p 2: 1000, else 2000)")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--cpu-sample", type=int, default=512)
+    ap.add_argument("--warm-gens", type=int, default=0, help="at most this many untimed generations first")
+    ap.add_argument("--warm-feasible", type=float, default=1.1, help="stop warming once this fraction is feasible")
+    ap.add_argument("--lpt", choices=["auto", "on", "off"], default="auto",
+                    help="longest-expected-first dispatch of the children's local search (Island default: auto)")
+    ap.add_argument("--lib", default=None, help="profiling: an A/B build (tools/ab_build.sh) instead of the in-tree library")
+    return ap
+
+
+def run_ga(a):
+    """One island on the in-tree (or --lib) library; returns the JSON record."""
+    inst = ttga.config_instance(a.config)
+    dp = native.DeviceProblem(inst)
+    isl = Island(dp, pop_size=a.pop, children=a.children, max_steps=a.steps, seed=a.seed,
+                 lpt=None if a.lpt == "auto" else a.lpt == "on")
     torch.cuda.synchronize()
-    mism = [k for k in ("slot", "room", "hcv", "scv", "feasible", "penalty")
-            if not np.array_equal(c[k].cpu().numpy(), ref_children[k])]
-    if not np.array_equal(g.cpu().numpy(), ref_rng):
-        mism.append("rng")
-    out["children_match_reference"] = {"children": n, "match": not mism, "mismatched": mism,
-                                       "feasible_children": int(ref_children["feasible"].sum())}
-    out["cpu_baseline"] = {"kind": "reference", "cores": threads, "cpu_model": model, "host_cores_total": total,
-                           "sample_children": n, "seconds": res[0],
-                           "children_per_s": n / res[0],
-                           "what": "ga.cpp:543-577 per child (3x RandomInitialSolution, 2x selection5, copies, "
-                                   "crossover into a fresh child / copy, mutation, localSearch, computePenalty), "
-                                   "OpenMP over children",
-                           "as_is_children_per_s": n / res[1],
-                           "as_is_note": "crossover into the child that already holds a random solution, as "
-                                         "ga.cpp:543-563 does (SURVEY F2); its doubled slot lists change the "
-                                         "local search's work; context only, not used for the speedup"}
-    out["speedup_vs_cpu"] = out["gpu_children_per_s"] / out["cpu_baseline"]["children_per_s"]
-print(json.dumps(out))
+    t0 = time.perf_counter()
+    isl.initialize()
+    torch.cuda.synchronize()
+    init_s = time.perf_counter() - t0
+    isl.step()                                  # warm-up generation
+    torch.cuda.synchronize()
+    warm = 1
+    while warm < a.warm_gens and float(isl.pop["feasible"].float().mean().item()) < a.warm_feasible:
+        isl.step()
+        warm += 1
+    feas_start = float(isl.pop["feasible"].float().mean().item())
+    torch.cuda.synchronize()
+    # snapshot of the population and child streams the CPU sample (and its device replay) breed from
+    pop_slot, pop_room = isl.pop["slot"].cpu().numpy().copy(), isl.pop["room"].cpu().numpy().copy()
+    pop_pen = isl.pop["penalty"].cpu().numpy().copy()
+    snap = {k: v.clone() for k, v in isl.pop.items()}
+    snap_rng = isl.rng_child.clone()
+    t0 = time.perf_counter()
+    gens = 0
+    while gens < a.gens or time.perf_counter() - t0 < a.min_seconds:
+        isl.step()
+        gens += 1
+        # the generations are stream-ordered and need no host round trip; the clock is
+        # checked against the device every 8 generations (a sync after every one left
+        # the GPU idle while the host enqueued the next generation's launches)
+        if gens >= a.gens and gens % 8 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    gpu_s = time.perf_counter() - t0
+    feas, scv, hcv, pen = isl.member_meta(0)
+    # digest of the final population (slots, rooms, penalties): equal runs, equal digests
+    _h = hashlib.sha256()
+    for _k in ("slot", "room", "penalty"):
+        _h.update(isl.pop[_k].cpu().numpy().tobytes())
+    pop_digest = _h.hexdigest()[:16]
+    pf = isl.pop["feasible"].bool()
+    out = {"config": a.config, "E": inst.E, "R": inst.R, "F": inst.F, "S": inst.S, "pop": a.pop,
+           "children_per_gen": a.children, "gens": gens, "max_steps": a.steps, "lpt_dispatch": isl.lpt,
+           "init_seconds": init_s,
+           "warm_gens": warm, "feasible_fraction_at_start": feas_start,
+           "pop_digest": pop_digest, "gpu_seconds": gpu_s, "gpu_children_per_s": a.children * gens / gpu_s,
+           "best_scv_feasible": int(isl.pop["scv"][pf].min().item()) if bool(pf.any()) else None,
+           "best": {"feasible": feas, "scv": scv, "hcv": hcv, "penalty": pen},
+           "feasible_fraction": float(isl.pop["feasible"].float().mean().item())}
+
+    R = ref()
+    if R is not None and a.cpu_sample > 0:
+        n = min(a.cpu_sample, a.children)
+        threads, total, model = host_cores()
+        h = R.problem(inst)
+        seeds = snap_rng[:n].cpu().numpy().copy()
+        res = {}
+        for as_is in (1, 0):       # as_is = 0 last: its children are the ones compared
+            ref_children, ref_rng, res[as_is] = h.ga_children(pop_slot, pop_room, pop_pen, seeds, a.steps, threads, as_is)
+        # the device replay of the same children from the snapshot
+        c = {k: torch.empty_like(v[:n]) for k, v in snap.items()}
+        g = torch.from_numpy(seeds).cuda()
+        fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        dp.ga_breed(snap["slot"], snap["room"], snap["penalty"], g, c["slot"], c["room"], fl, isl.p_cross, isl.p_mut, True)
+        dp.local_search(c["slot"], c["room"], g, a.steps)
+        dp.eval(c["slot"], c["room"], out=(c["hcv"], c["scv"], c["feasible"], c["penalty"]))
+        torch.cuda.synchronize()
+        mism = [k for k in ("slot", "room", "hcv", "scv", "feasible", "penalty")
+                if not np.array_equal(c[k].cpu().numpy(), ref_children[k])]
+        if not np.array_equal(g.cpu().numpy(), ref_rng):
+            mism.append("rng")
+        out["children_match_reference"] = {"children": n, "match": not mism, "mismatched": mism,
+                                           "feasible_children": int(ref_children["feasible"].sum())}
+        out["cpu_baseline"] = {"kind": "reference", "cores": threads, "cpu_model": model, "host_cores_total": total,
+                               "sample_children": n, "seconds": res[0],
+                               "children_per_s": n / res[0],
+                               "what": "ga.cpp:543-577 per child (3x RandomInitialSolution, 2x selection5, copies, "
+                                       "crossover into a fresh child / copy, mutation, localSearch, computePenalty), "
+                                       "OpenMP over children",
+                               "as_is_children_per_s": n / res[1],
+                               "as_is_note": "crossover into the child that already holds a random solution, as "
+                                             "ga.cpp:543-563 does (SURVEY F2); its doubled slot lists change the "
+                                             "local search's work; context only, not used for the speedup"}
+        out["speedup_vs_cpu"] = out["gpu_children_per_s"] / out["cpu_baseline"]["children_per_s"]
+    return out
+
+
+if __name__ == "__main__":
+    args = parser().parse_args()
+    if args.lib:
+        native._lib = native.load(pathlib.Path(args.lib).resolve())
+    print(json.dumps(run_ga(args)))

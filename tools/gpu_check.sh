@@ -114,7 +114,13 @@ for s in $STEPS; do
            run ga8k_comp15_check 300 python -u tools/bench_ga.py --config comp15 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 512 ;;
     lstests) run pytest_ls 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_ga.py tests/test_gpu_configs.py tests/test_gpu_baseline_configs.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
     gap1c) for i in 1 2; do for c in comp15 comp10 comp05 comp01; do for l in r5c0 r5c; do run ga8k_${c}_${l}_$i 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done; done ;;
+    gap1d) for i in 1 2; do for c in comp15 comp10 comp05 comp01; do for l in r5d0 r5d; do run ga8k_${c}_${l}_$i 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done; done ;;
+    abt5d) run ab_t5d_med 300 python -u tools/ab_eval.py med 65536 r5d:8 prio:8 r5d:9 r5d:8 prio:8 r5d:9 &&
+           run ab_t5d_lg 300 python -u tools/ab_eval.py lg 65536 r5d:8 prio:8 r5d:9 r5d:8 prio:8 r5d:9 &&
+           run ab_t5d_comp01 300 python -u tools/ab_eval.py comp01 65536 r5d:8 prio:8 r5d:9 r5d:8 prio:8 r5d:9 ;;
     t6abl) run t6_ablate 300 python -u tools/eval_variants.py med 65536 8,24,40,9,25,41 ;;
+    gacomps20) run ga_comps 900 python -u tools/ga_comps.py "$OUT/ga_comps.json" ;;
+    gatrace15) run ga8k_trace15 400 rocprofv3 --kernel-trace --stats -d "$OUT/ga_trace15" -o run --output-format csv -- python -u tools/bench_ga.py --config comp15 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 20 --cpu-sample 0 ;;
     selftest) run bench_self2 300 env TTGA_BENCH_BACKEND=gloo python -u bench.py --gpus 2 --steps 20 --warmup 2 --no-pmc --no-cpu ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python -u bench.py --no-pmc --no-cpu --steps 100 ;;
     *) echo "unknown step $s"; exit 2 ;;
