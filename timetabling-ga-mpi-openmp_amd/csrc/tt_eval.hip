@@ -472,6 +472,14 @@ __device__ __forceinline__ uint32_t mad_u16_hi(uint32_t a, uint32_t b, uint32_t 
 #ifndef TT_T5_PRIO
 #define TT_T5_PRIO 0
 #endif
+// the schedule: priority in the lane phase, then per individual i of the wave's
+// (up to 8) wave-phase individuals nibble i of TT_T5_PRIO_W
+#ifndef TT_T5_PRIO_LANE
+#define TT_T5_PRIO_LANE 3
+#endif
+#ifndef TT_T5_PRIO_W
+#define TT_T5_PRIO_W 0x11112222u
+#endif
 template <int EWC, int NW, int PK, bool DB = false>
 __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
                                                               const uint8_t* __restrict__ room, int P,
@@ -582,9 +590,8 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
         // kept live across the tile loop, the product spilled to scratch)
         uint32_t lsp;
         asm volatile("v_mul_u32_u24 %0, %1, %2" : "=v"(lsp) : "v"(lane), "s"(SP));
-        if (TT_T5_PRIO) __builtin_amdgcn_s_setprio(3);
+        if (TT_T5_PRIO) __builtin_amdgcn_s_setprio(TT_T5_PRIO_LANE);
         const int sc = (!(ablate & 1) && r0 < r1) ? lane_scv_runs<1>(tile + lsp, pb, r0, r1) : 0;
-        if (TT_T5_PRIO) __builtin_amdgcn_s_setprio(2);
         part[wv * 64 + lane] = sc;
 
         // ---- wave phase (wave = individual): hcv terms + last-slot term
@@ -613,7 +620,14 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
 #endif
         if (wv < nq) load_row(room, wv, pfn);
         for (int q = wv; q < nq; q += NW) {
-            if (TT_T5_PRIO && q == wv + 4 * NW) __builtin_amdgcn_s_setprio(1);
+            if (TT_T5_PRIO) {
+                // s_setprio takes an immediate: one of four, by the schedule's nibble
+                const uint32_t pr = (TT_T5_PRIO_W >> (4 * min((q - wv) / NW, 7))) & 3u;
+                if (pr == 0) __builtin_amdgcn_s_setprio(0);
+                else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+                else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+                else __builtin_amdgcn_s_setprio(3);
+            }
             uint32_t rv[EWC], sv[EWC];
 #pragma unroll
             for (int r = 0; r < EWC; ++r) rv[r] = pfn[r];

@@ -1349,7 +1349,10 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
         }
         const bool hotm = TT_LS_HOT && fast1 && 4 * nhot <= E;
         // many events in conflict: room-pair lower bounds before the matcher (TT_LS_P1B)
-        if (TT_LS_P1B && !hotm && fast1) {
+#ifndef TT_LS_P1B_RTOFF
+#define TT_LS_P1B_RTOFF 0       // profiling: the bounds compiled in but never enabled (p1 < 2 always)
+#endif
+        if (TT_LS_P1B && !hotm && fast1 && !(TT_LS_P1B_RTOFF && p1 < 2.0)) {
             S.sinf = (SlotInfo*)(lds + L.sinf);
             S.tsi = S.sinf + kSlots;
             S.nz = (int32_t*)(S.tsi + 3);

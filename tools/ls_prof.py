@@ -33,9 +33,10 @@ ap.add_argument("--from-ga", type=float, default=0.0,
                      "this fraction of it is feasible, then one generation's bred children are searched")
 ap.add_argument("--children", type=int, default=32768)
 ap.add_argument("--warm-gens", type=int, default=400, help="--from-ga: at most this many generations first")
+ap.add_argument("--lib", default=None, help="a profiling A/B build (tools/ab_build_one.sh with -DTT_LS_PROF)")
 a = ap.parse_args()
 
-lib = native.load(native.PKG_DIR / "libttga_prof.so")
+lib = native.load(pathlib.Path(a.lib).resolve() if a.lib else native.PKG_DIR / "libttga_prof.so")
 native._lib = lib
 lib.tt_ls_prof_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
 lib.tt_ls_prof_read.restype = ctypes.c_int
