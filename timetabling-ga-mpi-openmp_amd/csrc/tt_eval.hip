@@ -465,12 +465,14 @@ __device__ __forceinline__ uint32_t mad_u16_hi(uint32_t a, uint32_t b, uint32_t 
 }
 
 // TT_T5_PRIO: issue priority falls as a wave gets through its tile (3 in the
-// lane phase, 2 for its first half of individuals, 1 after), so of a CU's two
-// resident workgroups the one further behind wins the arbiter -- instead of
-// the older one (round-4 stamps: the older finishes 31.9 us, its neighbour
-// 43.0 us, and the CU's last workgroup runs alone for 15 us).
+// lane phase, then 3, 3, 2, 2, 1, 1, 0, 0 over its wave-phase individuals), so
+// of a CU's two resident workgroups the one further behind wins the arbiter --
+// instead of the older one (round-4 stamps: the older finishes 31.9 us, its
+// neighbour 43.0 us, and the CU's last workgroup runs alone for 15 us). Same
+// box (gpurun_out/r05_e/ab_prio_*.log): med 74.2 -> 71.8 us, lg 96.9 -> 94.1,
+// comp01 100.0 -> 100.1; slower decays measured 72.1-73.1 us at med.
 #ifndef TT_T5_PRIO
-#define TT_T5_PRIO 0
+#define TT_T5_PRIO 1
 #endif
 // the schedule: priority in the lane phase, then per individual i of the wave's
 // (up to 8) wave-phase individuals nibble i of TT_T5_PRIO_W
@@ -478,7 +480,7 @@ __device__ __forceinline__ uint32_t mad_u16_hi(uint32_t a, uint32_t b, uint32_t 
 #define TT_T5_PRIO_LANE 3
 #endif
 #ifndef TT_T5_PRIO_W
-#define TT_T5_PRIO_W 0x11112222u
+#define TT_T5_PRIO_W 0x00112233u
 #endif
 template <int EWC, int NW, int PK, bool DB = false>
 __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, const uint8_t* __restrict__ slot,

@@ -177,19 +177,21 @@ struct LsState {
     // phase 2: the state stays feasible, so every slot's rooms are distinct and
     // hist[] is reused as the owner table oe[slot * R + room] (event, 0xFFFF free)
     int phase2;
-    // phase-1 pair bounds (TT_LS_P1B): per-slot matching summaries (sinf, nz) and
-    // npw (lane w) = word w of the events without a possible room. Null sinf: off.
+    // phase-1 pair bounds (TT_LS_P1B): per-slot matching summaries; null sinf: off.
+    // One base pointer (fewer live registers in the whole kernel): sinf[45], then the
+    // tasks' tsi[3], nz[45] (N << 16 | Z, bit 31: the summary is of a maximum matching),
+    // the tasks' tnz[3], and own[64] (scratch: the owner of each room while a summary is built)
     SlotInfo* sinf;
-    int32_t* nz;         // [45] N << 16 | Z, bit 31: the summary is of a maximum matching
-    uint16_t* own;       // [64] scratch: the owner of each room while a summary is built
-    SlotInfo* tsi;       // [3] summaries of the matcher tasks' slots (the wave matcher's result)
-    int32_t* tnz;        // [3]
     int tvalid;          // bit k: tsi[k] / tnz[k] describe the current neighbour's task k
-    uint64_t npw;
 #ifdef TT_LS_PROF
     uint64_t prof[kPfN];
 #endif
 };
+
+__device__ __forceinline__ SlotInfo* tsi_of(const LsState& S) { return S.sinf + kSlots; }
+__device__ __forceinline__ int32_t* nz_of(const LsState& S) { return (int32_t*)(S.sinf + kSlots + 3); }
+__device__ __forceinline__ int32_t* tnz_of(const LsState& S) { return nz_of(S) + kSlots; }
+__device__ __forceinline__ uint16_t* own_of(const LsState& S) { return (uint16_t*)(nz_of(S) + kSlots + 3); }
 
 __device__ __forceinline__ LsTask get_task(const LsState& S, int k) {
     uint8_t* tb = S.task_base + (size_t)k * S.task_bytes;
@@ -499,9 +501,9 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
         }
         const int z = __popcll(ballot(act && pl == 0ull));
         if (lane == 0) {
-            S.tsi[k].used = rmatched;
-            S.tsi[k].fr = fr;
-            S.tnz[k] = (int)0x80000000 | (N << 16) | z;
+            tsi_of(S)[k].used = rmatched;
+            tsi_of(S)[k].fr = fr;
+            tnz_of(S)[k] = (int)0x80000000 | (N << 16) | z;
         }
         S.tvalid |= 1 << k;
     }
@@ -802,7 +804,7 @@ __device__ __forceinline__ void accept(LsState& S) {
         for (int k = 0; k < 3; ++k) {
             if (k >= S.nts) break;
             if ((S.tvalid >> k) & 1) {                     // from the wave matcher's own result
-                if (S.lane == 0) { S.sinf[S.ts[k]] = S.tsi[k]; S.nz[S.ts[k]] = S.tnz[k]; }
+                if (S.lane == 0) { S.sinf[S.ts[k]] = tsi_of(S)[k]; nz_of(S)[S.ts[k]] = tnz_of(S)[k]; }
             } else {
                 sinf_build(S, S.ts[k]);
             }
@@ -992,17 +994,17 @@ __device__ __forceinline__ bool matchable(LsState& S, int s, int out, int a) {
 // value is rejected exactly as its full evaluation would reject it.
 __device__ __forceinline__ void sinf_build(LsState& S, int t) {
     const int R = S.R, EW = S.EW, lane = S.lane;
-    if (lane < R) S.own[lane] = 0xFFFF;
+    if (lane < R) own_of(S)[lane] = 0xFFFF;
     wave_sync();
     for (int w = 0; w < EW; ++w) {
         const int e = 64 * w + lane;
         if ((S.B[(size_t)t * EW + w] >> lane) & 1ull) {
             const int r = S.rr[e];
-            if ((poss_of(S, e) >> r) & 1ull) S.own[r] = (uint16_t)e;
+            if ((poss_of(S, e) >> r) & 1ull) own_of(S)[r] = (uint16_t)e;
         }
     }
     wave_sync();
-    const int o = lane < R ? (int)S.own[lane] : 0xFFFF;
+    const int o = lane < R ? (int)own_of(S)[lane] : 0xFFFF;
     const bool valid = o != 0xFFFF;
     const uint64_t po = valid ? poss_of(S, o) : 0ull;
     const uint64_t used = ballot(valid);
@@ -1018,15 +1020,17 @@ __device__ __forceinline__ void sinf_build(LsState& S, int t) {
     for (int w = 0; w < EW; ++w) {
         const uint64_t bw = S.B[(size_t)t * EW + w];
         n += __popcll(bw);
-        z += __popcll(bw & readlane64(S.npw, w));
         const int e = 64 * w + lane;
-        if ((bw >> lane) & 1ull) aug |= S.own[S.rr[e]] != e && (poss_of(S, e) & fr) != 0ull;
+        const bool in = (bw >> lane) & 1ull;
+        const uint64_t pe = in ? poss_of(S, e) : 1ull;
+        z += __popcll(ballot(pe == 0ull));
+        if (in) aug |= own_of(S)[S.rr[e]] != e && (pe & fr) != 0ull;
     }
     const bool trusted = !wave_any(aug);
     if (lane == 0) {
         S.sinf[t].used = used;
         S.sinf[t].fr = fr;
-        S.nz[t] = (trusted ? (int)0x80000000 : 0) | (n << 16) | z;
+        nz_of(S)[t] = (trusted ? (int)0x80000000 : 0) | (n << 16) | z;
     }
     wave_sync();
 }
@@ -1041,7 +1045,7 @@ __device__ __forceinline__ int pairs_lb_of(const SlotInfo& I, int nz, uint64_t p
     return u > 0 ? u : 0;
 }
 __device__ __forceinline__ int pairs_lb(LsState& S, int s, int out, int a) {
-    return pairs_lb_of(S.sinf[s], S.nz[s], poss_of(S, a), out >= 0 ? poss_of(S, out) : 0ull, out >= 0);
+    return pairs_lb_of(S.sinf[s], nz_of(S)[s], poss_of(S, a), out >= 0 ? poss_of(S, out) : 0ull, out >= 0);
 }
 
 // start of phase 1: the no-room event words and every slot's summary, all
@@ -1052,12 +1056,6 @@ __device__ __forceinline__ int pairs_lb(LsState& S, int s, int out, int a) {
 __device__ __forceinline__ void sinf_init(LsState& S) {
     LSP_T(t0);
     const int E = S.E, R = S.R, lane = S.lane;
-    S.npw = 0;
-    for (int k = 0; 64 * k < E; ++k) {                          // wave-uniform
-        const int e = 64 * k + lane;
-        const uint64_t m = ballot(e < E && poss_of(S, e) == 0ull);
-        if (lane == k) S.npw = m;
-    }
     const int NC = kSlots * R;
     if ((size_t)2 * NC > (size_t)kLsTasks * S.task_bytes) {
         for (int t = 0; t < kSlots; ++t) sinf_build(S, t);
@@ -1068,13 +1066,13 @@ __device__ __forceinline__ void sinf_init(LsState& S) {
     const uint64_t rmask = R >= 64 ? ~0ull : ((1ull << R) - 1);
     const uint32_t rinv = ((1u << 20) + (uint32_t)R - 1) / (uint32_t)R;   // c / R = (c * rinv) >> 20 for c < 2^12
     for (int c = lane; c < NC; c += 64) own2[c] = 0xFFFF;
-    if (lane < kSlots) { S.sinf[lane].used = 0ull; S.nz[lane] = (int)0x80000000; }
+    if (lane < kSlots) { S.sinf[lane].used = 0ull; nz_of(S)[lane] = (int)0x80000000; }
     wave_sync();
     for (int e = lane; e < E; e += 64) {
         const int t = S.sl[e], r = S.rr[e];
         const uint64_t pe = poss_of(S, e);
         if ((pe >> r) & 1ull) own2[t * R + r] = (uint16_t)e;
-        atomicAdd(&S.nz[t], (1 << 16) | (pe == 0ull ? 1 : 0));
+        atomicAdd(&nz_of(S)[t], (1 << 16) | (pe == 0ull ? 1 : 0));
     }
     wave_sync();
     for (int c = lane; c < NC; c += 64) {
@@ -1101,7 +1099,7 @@ __device__ __forceinline__ void sinf_init(LsState& S) {
     for (int e = lane; e < E; e += 64) {                        // Berge: no unmatched event reaches a free room
         const int t = S.sl[e];
         const uint64_t pe = poss_of(S, e);
-        if (pe != 0ull && own2[t * R + S.rr[e]] != e && (pe & S.sinf[t].fr) != 0ull) atomicAnd(&S.nz[t], 0x7FFFFFFF);
+        if (pe != 0ull && own2[t * R + S.rr[e]] != e && (pe & S.sinf[t].fr) != 0ull) atomicAnd(&nz_of(S)[t], 0x7FFFFFFF);
     }
     wave_sync();
     LSP_ADD(S, kPfBInit, t0);
@@ -1233,8 +1231,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     S.c1_valid = 0;
     S.listed = 0;
     S.phase2 = 0;
-    S.sinf = nullptr; S.nz = nullptr; S.own = nullptr; S.npw = 0;
-    S.tsi = nullptr; S.tnz = nullptr; S.tvalid = 0;
+    S.sinf = nullptr; S.tvalid = 0;
 #ifdef TT_LS_PROF
 #pragma unroll
     for (int i = 0; i < kPfN; ++i) S.prof[i] = 0;
@@ -1354,10 +1351,6 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
 #endif
         if (TT_LS_P1B && !hotm && fast1 && !(TT_LS_P1B_RTOFF && p1 < 2.0)) {
             S.sinf = (SlotInfo*)(lds + L.sinf);
-            S.tsi = S.sinf + kSlots;
-            S.nz = (int32_t*)(S.tsi + 3);
-            S.tnz = S.nz + kSlots;
-            S.own = (uint16_t*)(S.tnz + 3);
             sinf_init(S);
         }
         for (int i = 0; evc < E; i = wrap_e(i + 1, E)) {
@@ -1421,7 +1414,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                     const int tk = (t_start + h + lane) % kSlots;
                     const int xt = bperm(V.x, tk);                          // every lane takes part
                     // with the pair bound of slot tk plus ei (TT_LS_P1B) when the summaries are kept
-                    const int ub = S.sinf ? pairs_lb_of(S.sinf[tk], S.nz[tk], pei, 0ull, false) : 0;
+                    const int ub = S.sinf ? pairs_lb_of(S.sinf[tk], nz_of(S)[tk], pei, 0ull, false) : 0;
                     const bool skip = tk != t_orig && xt + S.misc[1] + ub >= eah_i + S.rp[tk];
                     const bool need = lane < rem && !skip;
                     bool done;
@@ -1506,8 +1499,8 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                             int lb = xt - cij + c2;
                             if (S.sinf) {                          // pair bounds of both touched slots
                                 const uint64_t pej = poss_of(S, ej);
-                                lb += pairs_lb_of(S.sinf[tj], S.nz[tj], pei, pej, true) +
-                                      pairs_lb_of(S.sinf[t_orig], S.nz[t_orig], pej, pei, true);
+                                lb += pairs_lb_of(S.sinf[tj], nz_of(S)[tj], pei, pej, true) +
+                                      pairs_lb_of(S.sinf[t_orig], nz_of(S)[t_orig], pej, pei, true);
                             }
                             need = lb < c;
                         }
