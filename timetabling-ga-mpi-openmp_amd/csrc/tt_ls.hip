@@ -57,7 +57,7 @@ __device__ unsigned long long g_ls_prof[kPfN];
 #endif
 
 struct LsLayout {
-    size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, cnt, task, slp, pos, ps, sm, sinf;
+    size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, task, slp, pos, ps, sm, sinf;
     size_t task_bytes;
     int NT;              // events per matcher task (min(E, 256))
     size_t bytes;
@@ -90,12 +90,16 @@ constexpr size_t kSmaskMaxBytes = 4096;
 #ifndef TT_LS_P1B
 #define TT_LS_P1B 1
 #endif
+// (R <= 16: the room sets fit 16 bits, a summary 8 bytes)
 struct SlotInfo {
-    uint64_t used;       // rooms matched in a maximum matching of the slot
-    uint64_t fr;         // rooms from which an alternating path reaches a free room (free rooms included)
+    uint16_t used;       // rooms matched in a maximum matching of the slot
+    uint16_t fr;         // rooms from which an alternating path reaches a free room (free rooms included)
+    int32_t nz;          // N << 16 | Z (events; events without a possible room), bit 31: trusted
 };
-// SlotInfo[45], the matcher tasks' SlotInfo[3], nz[45] (N << 16 | Z, bit 31: trusted), the tasks' nz[3], owners[64]
-constexpr size_t kSinfBytes = 16 * (kSlots + 3) + 4 * (kSlots + 3) + 128;
+constexpr int kP1bMaxRooms = 16;
+// SlotInfo[45] of the slots, then [3] of the matcher tasks: 384 B per wave, in the
+// phase-2 student-mask region when there is one (the two phases never overlap)
+constexpr size_t kSinfBytes = sizeof(SlotInfo) * (kSlots + 3);
 // cap: events per matcher task (kLsCapSmall for the first launch, kMaxSlotEvents for the redo launch)
 // S: students with phase-2 masks (0: none)
 __host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap, int S) {
@@ -127,9 +131,13 @@ __host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap, int
     L.NB = b; b += 8 * (size_t)kLsTasks * EW;
     L.rp = b; b += 4 * (size_t)kSlots;
     L.hist = b; b += 2 * (size_t)kSlots * R;
-    al(8); L.sinf = b; if (TT_LS_P1B) b += kSinfBytes;                  // phase-1 slot summaries
+    // phase-1 slot summaries: aliased with the phase-2 student masks when those exist
+    L.sinf = 0;
+    if (TT_LS_P1B && R <= kP1bMaxRooms) {
+        if (L.sm && S > 0 && 8 * (size_t)S <= kSmaskMaxBytes && 8 * (size_t)S >= kSinfBytes) L.sinf = L.sm;
+        else { al(8); L.sinf = b; b += kSinfBytes; }
+    }
     al(4); L.misc = b; b += 4 * 32;
-    L.cnt = b; b += 4 * (size_t)kMaxRooms;
     L.NT = E < cap ? E : cap;
     size_t tb = 11 * (size_t)L.NT + 1 + 4 * (size_t)R;   // pl, ev, mr, (pad), hist, rm, dr
     L.task_bytes = (tb + 15) & ~(size_t)15;
@@ -163,7 +171,6 @@ struct LsState {
     int32_t* rp;
     uint16_t* hist;
     int32_t* misc;       // [0..2] neighbour room pairs per task, [3] redo flag, [4..6] events per task
-    uint32_t* cnt;       // [R] room counters of the task being read out
     uint8_t* task_base;
     int task_bytes, NT;
     // neighbour description (wave-uniform)
@@ -178,20 +185,15 @@ struct LsState {
     // hist[] is reused as the owner table oe[slot * R + room] (event, 0xFFFF free)
     int phase2;
     // phase-1 pair bounds (TT_LS_P1B): per-slot matching summaries; null sinf: off.
-    // One base pointer (fewer live registers in the whole kernel): sinf[45], then the
-    // tasks' tsi[3], nz[45] (N << 16 | Z, bit 31: the summary is of a maximum matching),
-    // the tasks' tnz[3], and own[64] (scratch: the owner of each room while a summary is built)
+    // one base pointer: sinf[45] of the slots, then tsi[3] of the matcher tasks
     SlotInfo* sinf;
-    int tvalid;          // bit k: tsi[k] / tnz[k] describe the current neighbour's task k
+    int tvalid;          // bit k: tsi[k] describes the current neighbour's task k
 #ifdef TT_LS_PROF
     uint64_t prof[kPfN];
 #endif
 };
 
 __device__ __forceinline__ SlotInfo* tsi_of(const LsState& S) { return S.sinf + kSlots; }
-__device__ __forceinline__ int32_t* nz_of(const LsState& S) { return (int32_t*)(S.sinf + kSlots + 3); }
-__device__ __forceinline__ int32_t* tnz_of(const LsState& S) { return nz_of(S) + kSlots; }
-__device__ __forceinline__ uint16_t* own_of(const LsState& S) { return (uint16_t*)(nz_of(S) + kSlots + 3); }
 
 __device__ __forceinline__ LsTask get_task(const LsState& S, int k) {
     uint8_t* tb = S.task_base + (size_t)k * S.task_bytes;
@@ -501,9 +503,9 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
         }
         const int z = __popcll(ballot(act && pl == 0ull));
         if (lane == 0) {
-            tsi_of(S)[k].used = rmatched;
-            tsi_of(S)[k].fr = fr;
-            tnz_of(S)[k] = (int)0x80000000 | (N << 16) | z;
+            tsi_of(S)[k].used = (uint16_t)rmatched;
+            tsi_of(S)[k].fr = (uint16_t)fr;
+            tsi_of(S)[k].nz = (int)0x80000000 | (N << 16) | z;
         }
         S.tvalid |= 1 << k;
     }
@@ -804,7 +806,7 @@ __device__ __forceinline__ void accept(LsState& S) {
         for (int k = 0; k < 3; ++k) {
             if (k >= S.nts) break;
             if ((S.tvalid >> k) & 1) {                     // from the wave matcher's own result
-                if (S.lane == 0) { S.sinf[S.ts[k]] = tsi_of(S)[k]; nz_of(S)[S.ts[k]] = tnz_of(S)[k]; }
+                if (S.lane == 0) S.sinf[S.ts[k]] = tsi_of(S)[k];
             } else {
                 sinf_build(S, S.ts[k]);
             }
@@ -992,21 +994,41 @@ __device__ __forceinline__ bool matchable(LsState& S, int s, int out, int a) {
 // until an accepted move re-matches it with the reference matcher. A trial
 // whose correlation bound plus these pair bounds already reaches the current
 // value is rejected exactly as its full evaluation would reject it.
-__device__ __forceinline__ void sinf_build(LsState& S, int t) {
-    const int R = S.R, EW = S.EW, lane = S.lane;
-    if (lane < R) own_of(S)[lane] = 0xFFFF;
+// The summaries are built out of line (plain arguments: a reference to LsState
+// would put it in scratch): once per phase 1 and for a slot the lane-serial
+// matcher re-matched, so their code stays out of the trial loops (the kernel's
+// code grew 115 -> 136 KB with them inlined at every accept).
+struct SinfView {
+    SlotInfo* sinf;
+    const uint64_t* B;
+    const uint8_t* sl;
+    const uint8_t* rr;
+    const uint16_t* ps;
+    const uint64_t* poss;
+    uint8_t* task_base;
+    int E, R, EW, task_bytes;
+};
+__device__ __forceinline__ SinfView sinf_view(const LsState& S) {
+    return SinfView{S.sinf, S.B, S.sl, S.rr, S.ps, S.pb.poss, S.task_base, S.E, S.R, S.EW, S.task_bytes};
+}
+__device__ __forceinline__ uint64_t vposs(const SinfView& V, int e) { return V.ps ? (uint64_t)V.ps[e] : V.poss[e]; }
+
+__device__ __noinline__ void sinf_build_v(SinfView V, int t) {
+    const int R = V.R, EW = V.EW, lane = threadIdx.x & 63;
+    uint16_t* own = (uint16_t*)V.task_base;               // scratch: free after accept's hist copies
+    if (lane < R) own[lane] = 0xFFFF;
     wave_sync();
     for (int w = 0; w < EW; ++w) {
         const int e = 64 * w + lane;
-        if ((S.B[(size_t)t * EW + w] >> lane) & 1ull) {
-            const int r = S.rr[e];
-            if ((poss_of(S, e) >> r) & 1ull) own_of(S)[r] = (uint16_t)e;
+        if ((V.B[(size_t)t * EW + w] >> lane) & 1ull) {
+            const int r = V.rr[e];
+            if ((vposs(V, e) >> r) & 1ull) own[r] = (uint16_t)e;
         }
     }
     wave_sync();
-    const int o = lane < R ? (int)own_of(S)[lane] : 0xFFFF;
+    const int o = lane < R ? (int)own[lane] : 0xFFFF;
     const bool valid = o != 0xFFFF;
-    const uint64_t po = valid ? poss_of(S, o) : 0ull;
+    const uint64_t po = valid ? vposs(V, o) : 0ull;
     const uint64_t used = ballot(valid);
     uint64_t fr = (R >= 64 ? ~0ull : ((1ull << R) - 1)) & ~used;
     for (;;) {                                            // least fixed point, <= R rounds
@@ -1018,34 +1040,36 @@ __device__ __forceinline__ void sinf_build(LsState& S, int t) {
     int n = 0, z = 0;
     bool aug = false;
     for (int w = 0; w < EW; ++w) {
-        const uint64_t bw = S.B[(size_t)t * EW + w];
+        const uint64_t bw = V.B[(size_t)t * EW + w];
         n += __popcll(bw);
         const int e = 64 * w + lane;
         const bool in = (bw >> lane) & 1ull;
-        const uint64_t pe = in ? poss_of(S, e) : 1ull;
+        const uint64_t pe = in ? vposs(V, e) : 1ull;
         z += __popcll(ballot(pe == 0ull));
-        if (in) aug |= own_of(S)[S.rr[e]] != e && (pe & fr) != 0ull;
+        if (in) aug |= own[V.rr[e]] != e && (pe & fr) != 0ull;
     }
     const bool trusted = !wave_any(aug);
     if (lane == 0) {
-        S.sinf[t].used = used;
-        S.sinf[t].fr = fr;
-        nz_of(S)[t] = (trusted ? (int)0x80000000 : 0) | (n << 16) | z;
+        V.sinf[t].used = (uint16_t)used;
+        V.sinf[t].fr = (uint16_t)fr;
+        V.sinf[t].nz = (trusted ? (int)0x80000000 : 0) | (n << 16) | z;
     }
     wave_sync();
 }
+__device__ __forceinline__ void sinf_build(LsState& S, int t) { sinf_build_v(sinf_view(S), t); }
 
 // lower bound on the clash pairs of slot s minus `out` (-1: none) plus event a
 // after the reference's re-match (0 for an untrusted slot); any lanes
-__device__ __forceinline__ int pairs_lb_of(const SlotInfo& I, int nz, uint64_t pa, uint64_t pout, bool has_out) {
+__device__ __forceinline__ int pairs_lb_of(const SlotInfo& I, uint64_t pa, uint64_t pout, bool has_out) {
+    const int nz = I.nz;
     if (nz >= 0) return 0;                                     // bit 31 clear: untrusted
     const int N = ((nz >> 16) & 0x7FFF) + (has_out ? 0 : 1);
     const int Z = (nz & 0xFFFF) + (pa == 0ull) - (has_out && pout == 0ull);
-    const int u = N - __popcll(I.used) - ((pa & I.fr) != 0ull) - Z;
+    const int u = N - __popc((uint32_t)I.used) - ((pa & (uint64_t)I.fr) != 0ull) - Z;
     return u > 0 ? u : 0;
 }
 __device__ __forceinline__ int pairs_lb(LsState& S, int s, int out, int a) {
-    return pairs_lb_of(S.sinf[s], nz_of(S)[s], poss_of(S, a), out >= 0 ? poss_of(S, out) : 0ull, out >= 0);
+    return pairs_lb_of(S.sinf[s], poss_of(S, a), out >= 0 ? poss_of(S, out) : 0ull, out >= 0);
 }
 
 // start of phase 1: the no-room event words and every slot's summary, all
@@ -1053,43 +1077,41 @@ __device__ __forceinline__ int pairs_lb(LsState& S, int s, int out, int a) {
 // (free at this point), then the used masks, the fr fixed point over all
 // slots together, and the maximality check (sinf_build slot by slot when
 // the 45 x R owner table does not fit the task scratch)
-__device__ __forceinline__ void sinf_init(LsState& S) {
-    LSP_T(t0);
-    const int E = S.E, R = S.R, lane = S.lane;
+__device__ __noinline__ void sinf_init_v(SinfView V) {
+    const int E = V.E, R = V.R, lane = threadIdx.x & 63;
     const int NC = kSlots * R;
-    if ((size_t)2 * NC > (size_t)kLsTasks * S.task_bytes) {
-        for (int t = 0; t < kSlots; ++t) sinf_build(S, t);
-        LSP_ADD(S, kPfBInit, t0);
+    if ((size_t)2 * NC > (size_t)kLsTasks * V.task_bytes) {
+        for (int t = 0; t < kSlots; ++t) sinf_build_v(V, t);
         return;
     }
-    uint16_t* own2 = (uint16_t*)S.task_base;                    // [45][R]
+    uint16_t* own2 = (uint16_t*)V.task_base;                    // [45][R]
     const uint64_t rmask = R >= 64 ? ~0ull : ((1ull << R) - 1);
     const uint32_t rinv = ((1u << 20) + (uint32_t)R - 1) / (uint32_t)R;   // c / R = (c * rinv) >> 20 for c < 2^12
     for (int c = lane; c < NC; c += 64) own2[c] = 0xFFFF;
-    if (lane < kSlots) { S.sinf[lane].used = 0ull; nz_of(S)[lane] = (int)0x80000000; }
+    if (lane < kSlots) { V.sinf[lane].used = 0; V.sinf[lane].fr = 0; V.sinf[lane].nz = (int)0x80000000; }
     wave_sync();
     for (int e = lane; e < E; e += 64) {
-        const int t = S.sl[e], r = S.rr[e];
-        const uint64_t pe = poss_of(S, e);
+        const int t = V.sl[e], r = V.rr[e];
+        const uint64_t pe = vposs(V, e);
         if ((pe >> r) & 1ull) own2[t * R + r] = (uint16_t)e;
-        atomicAdd(&nz_of(S)[t], (1 << 16) | (pe == 0ull ? 1 : 0));
+        atomicAdd(&V.sinf[t].nz, (1 << 16) | (pe == 0ull ? 1 : 0));
     }
     wave_sync();
     for (int c = lane; c < NC; c += 64) {
         const int t = (int)(((uint32_t)c * rinv) >> 20), r = c - t * R;
-        if (own2[c] != 0xFFFF) atomicOr((unsigned long long*)&S.sinf[t].used, 1ull << r);
+        if (own2[c] != 0xFFFF) atomicOr((uint32_t*)&V.sinf[t], 1u << r);          // used: low half
     }
     wave_sync();
-    if (lane < kSlots) S.sinf[lane].fr = rmask & ~S.sinf[lane].used;
+    if (lane < kSlots) V.sinf[lane].fr = (uint16_t)(rmask & ~(uint64_t)V.sinf[lane].used);
     wave_sync();
     for (;;) {                                                  // fr of every slot, least fixed point
         bool ch = false;
         for (int c = lane; c < NC; c += 64) {
             const int t = (int)(((uint32_t)c * rinv) >> 20), r = c - t * R;
             const int o = own2[c];
-            const uint64_t f = S.sinf[t].fr;
-            if (o != 0xFFFF && !((f >> r) & 1ull) && (poss_of(S, o) & f) != 0ull) {
-                atomicOr((unsigned long long*)&S.sinf[t].fr, 1ull << r);
+            const uint64_t f = V.sinf[t].fr;                   // (atomics below touch the high half only)
+            if (o != 0xFFFF && !((f >> r) & 1ull) && (vposs(V, o) & f) != 0ull) {
+                atomicOr((uint32_t*)&V.sinf[t], 1u << (16 + r));                     // fr: high half
                 ch = true;
             }
         }
@@ -1097,11 +1119,16 @@ __device__ __forceinline__ void sinf_init(LsState& S) {
         if (!wave_any(ch)) break;
     }
     for (int e = lane; e < E; e += 64) {                        // Berge: no unmatched event reaches a free room
-        const int t = S.sl[e];
-        const uint64_t pe = poss_of(S, e);
-        if (pe != 0ull && own2[t * R + S.rr[e]] != e && (pe & S.sinf[t].fr) != 0ull) atomicAnd(&nz_of(S)[t], 0x7FFFFFFF);
+        const int t = V.sl[e];
+        const uint64_t pe = vposs(V, e);
+        if (pe != 0ull && own2[t * R + V.rr[e]] != e && (pe & (uint64_t)V.sinf[t].fr) != 0ull)
+            atomicAnd(&V.sinf[t].nz, 0x7FFFFFFF);
     }
     wave_sync();
+}
+__device__ __forceinline__ void sinf_init(LsState& S) {
+    LSP_T(t0);
+    sinf_init_v(sinf_view(S));
     LSP_ADD(S, kPfBInit, t0);
 }
 
@@ -1223,7 +1250,6 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     S.sm = nullptr;
     S.rp = (int32_t*)(lds + L.rp); S.hist = (uint16_t*)(lds + L.hist);
     S.misc = (int32_t*)(lds + L.misc);
-    S.cnt = (uint32_t*)(lds + L.cnt);
     S.task_base = lds + L.task;
     S.task_bytes = (int)L.task_bytes;
     S.NT = L.NT;
@@ -1349,7 +1375,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
 #ifndef TT_LS_P1B_RTOFF
 #define TT_LS_P1B_RTOFF 0       // profiling: the bounds compiled in but never enabled (p1 < 2 always)
 #endif
-        if (TT_LS_P1B && !hotm && fast1 && !(TT_LS_P1B_RTOFF && p1 < 2.0)) {
+        if (TT_LS_P1B && R <= kP1bMaxRooms && !hotm && fast1 && !(TT_LS_P1B_RTOFF && p1 < 2.0)) {
             S.sinf = (SlotInfo*)(lds + L.sinf);
             sinf_init(S);
         }
@@ -1414,7 +1440,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                     const int tk = (t_start + h + lane) % kSlots;
                     const int xt = bperm(V.x, tk);                          // every lane takes part
                     // with the pair bound of slot tk plus ei (TT_LS_P1B) when the summaries are kept
-                    const int ub = S.sinf ? pairs_lb_of(S.sinf[tk], nz_of(S)[tk], pei, 0ull, false) : 0;
+                    const int ub = S.sinf ? pairs_lb_of(S.sinf[tk], pei, 0ull, false) : 0;
                     const bool skip = tk != t_orig && xt + S.misc[1] + ub >= eah_i + S.rp[tk];
                     const bool need = lane < rem && !skip;
                     bool done;
@@ -1499,8 +1525,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
                             int lb = xt - cij + c2;
                             if (S.sinf) {                          // pair bounds of both touched slots
                                 const uint64_t pej = poss_of(S, ej);
-                                lb += pairs_lb_of(S.sinf[tj], nz_of(S)[tj], pei, pej, true) +
-                                      pairs_lb_of(S.sinf[t_orig], nz_of(S)[t_orig], pej, pei, true);
+                                lb += pairs_lb_of(S.sinf[tj], pei, pej, true) + pairs_lb_of(S.sinf[t_orig], pej, pei, true);
                             }
                             need = lb < c;
                         }

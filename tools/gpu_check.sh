@@ -127,6 +127,7 @@ for s in $STEPS; do
              run ab_prio2_lg 400 python -u tools/ab_eval.py lg 65536 r5f:8 pG:8 pH:8 pI:8 r5f:8 pG:8 pH:8 pI:8 &&
              run ab_prio2_comp01 400 python -u tools/ab_eval.py comp01 65536 r5f:8 pG:8 pH:8 pI:8 r5f:8 pG:8 pH:8 pI:8 ;;
     gap1f) for i in 1 2; do for c in comp15 comp10 comp01; do for l in r5f0 r5f; do run ga8k_${c}_${l}_$i 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done; done ;;
+    gap1g) for i in 1 2; do for c in comp15 comp10 comp01; do for l in r5g0 r5g; do run ga8k_${c}_${l}_$i 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done; done ;;
     t6abl) run t6_ablate 300 python -u tools/eval_variants.py med 65536 8,24,40,9,25,41 ;;
     gacomps20) run ga_comps 900 python -u tools/ga_comps.py "$OUT/ga_comps.json" ;;
     gatrace15) run ga8k_trace15 400 rocprofv3 --kernel-trace --stats -d "$OUT/ga_trace15" -o run --output-format csv -- python -u tools/bench_ga.py --config comp15 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 20 --cpu-sample 0 ;;
