@@ -1379,234 +1379,15 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
             S.sinf = (SlotInfo*)(lds + L.sinf);
             sinf_init(S);
         }
-        for (int i = 0; evc < E; i = wrap_e(i + 1, E)) {
-            if (step > max_steps || ++guard > guard_max) break;
-            if (hotm) {
-                LSP_T(t_skip);
-                // jump to the next event with eventHcv > 0 (each one skipped is a visit
-                // that only counts towards evCount); the loop ends after E in a row
-                bool out = false;
-                for (;;) {
-                    const int rem = E - evc;                            // visits left before the loop ends
-                    int pk = i + lane;
-                    while (pk >= E) pk -= E;
-                    const int ek = S.evl[pk];
-                    const uint64_t hw = bperm64(hot, ek >> 6);
-                    const uint64_t hb = ballot(lane < rem && ((hw >> (ek & 63)) & 1ull));
-                    if (hb) {
-                        const int k = __builtin_ctzll(hb);
-                        evc += k; guard += k;
-                        i = wrap_e(i + k, E);
-                        break;
-                    }
-                    const int n = rem < 64 ? rem : 64;
-                    evc += n; guard += n;
-                    i = wrap_e(i + n, E);
-                    if (evc >= E) { out = true; break; }
-                }
-                LSP_ADD(S, kPfSkip1, t_skip);
-                if (out || guard > guard_max) break;
-            }
-            const int ei = S.evl[i];
-            LSP_CNT(S, kPfVisits);
-            LSP_T(t_vis);
-            uint64_t row = nrow;
-            if (fast1 && TT_LS_ROWPF) nrow = load_row(S, S.evl[i + 1 < E ? i + 1 : 0]);
-            else if (fast1) row = load_row(S, ei);
-            // eventHcv(ei) (Solution.cpp:173-191); known > 0 from the flags
-            const int ehcv = hotm ? 1
-                             : fast1 ? (int)S.hist[S.sl[ei] * R + S.rr[ei]] - 1 +
-                                           row_in_set(S, row, S.B + (size_t)S.sl[ei] * EW) - (int)row_bit(row, ei)
-                                     : ehcv_cur(S, ei);
-            if (ehcv == 0) { evc++; LSP_ADD(S, kPfVis1, t_vis); continue; }
-            const int t_orig = S.sl[ei];
-            Visit2 V;
-            if (fast1) visit2_x_from_row(S, row, V);
-            // eventAffectedHcv(ei) in the current state: unchanged until a trial is
-            // accepted, and every acceptance leaves this event's loops
-            const int eah_i = fast1 ? S.rp[t_orig] + __builtin_amdgcn_readlane(V.x, t_orig) - (int)row_bit(V.row, ei)
-                                    : eah_cur(S, ei);
-            const uint64_t pei = S.sinf ? poss_of(S, ei) : 0ull;        // for the pair bounds
-            LSP_ADD(S, kPfVis1, t_vis);
-            LSP_T(t_m1);
-            const int t_start = pm_pick(st, kSlots);
-            for (int h = 0; h < kSlots;) {
-                if (step > max_steps) break;
-                if (TT_LS_M1WIN && fast1 && S.c1_valid && (uint64_t)st < kPmM) {
-                    // window: lane k screens target t_start+h+k against the kept task's
-                    // bound X[t] + misc[1] >= c (the scalar test below is the same). Only
-                    // with the old-slot task kept: before that the first trial runs anyway
-                    const int rem = kSlots - h;
-                    const int tk = (t_start + h + lane) % kSlots;
-                    const int xt = bperm(V.x, tk);                          // every lane takes part
-                    // with the pair bound of slot tk plus ei (TT_LS_P1B) when the summaries are kept
-                    const int ub = S.sinf ? pairs_lb_of(S.sinf[tk], pei, 0ull, false) : 0;
-                    const bool skip = tk != t_orig && xt + S.misc[1] + ub >= eah_i + S.rp[tk];
-                    const bool need = lane < rem && !skip;
-                    bool done;
-                    const int ks = window_resolve(lane, jump, st, step, max_steps, rem, p1, need, done);
-                    if (ks == 64) break;                                // rem <= 45 < 64: the loop ends here
-                    h += ks;
-                } else {
-                    if (!(pm_next(st) < p1)) { h++; continue; }
-                    step++;
-                }
-                const int t = (t_start + h) % kSlots;
-                h++;
-                {
-                    const int c = eah_i + S.rp[t];
-                    // the kept old-slot task gives misc[1]; corr_nb(ei) in t is X[t]
-                    if (fast1 && S.c1_valid && t != t_orig && __builtin_amdgcn_readlane(V.x, t) + S.misc[1] >= c) continue;
-                    set_move(S, 1, ei, t, 0);
-                    build_nb(S);
-                    if (S.nts == 2) {
-                        // task 0 = t plus ei, task 1 = t_orig minus ei (kept across trials).
-                        // n = corr + misc[1] + misc[0] >= corr + misc[1]: a trial that cannot
-                        // win is rejected before the target slot is matched.
-#ifdef TT_LS_PROF
-                        if (!S.c1_valid) LSP_CNT(S, kPfP1m1k);
-#endif
-                        if (match_tasks(S, 2)) goto redo;
-                        const int lb = (fast1 ? __builtin_amdgcn_readlane(V.x, t) : corr_nb(S, ei)) + S.misc[1];
-                        if (lb >= c) { S.c1_valid = 1; continue; }
-                        if (S.sinf && lb + pairs_lb(S, t, -1, ei) >= c) { LSP_CNT(S, kPfB1); S.c1_valid = 1; continue; }
-                        LSP_CNT(S, kPfP1m1m);
-                        if (match_tasks(S, 1)) goto redo;
-                        if (lb + S.misc[0] < c) { LSP_CNT(S, kPfP1m1a); accept(S);
-                            if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
-                    } else {
-                        if (match_tasks(S, 7)) goto redo;
-                        const int n = eah_nb(S, ei) + S.misc[task_of(S, t_orig)];
-                        if (n < c) { accept(S);
-                            if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
-                    }
-                    reject_move1(S);
-                }
-            }
-            cache_drop(S);
-            LSP_ADD(S, kPfM1p1, t_m1);
-            if (better) { better = false; continue; }
-            if (p2 != 0) {
-                LSP_T(t_m2);
-                // B[t_orig] without ei: the partner's slot-mates after a swap
-                uint64_t bo = 0;
-                if (fast1 && lane < EW) {
-                    bo = S.B[(size_t)t_orig * EW + lane];
-                    if ((ei >> 6) == lane) bo &= ~(1ull << (ei & 63));
-                }
-                int j = wrap_e(i + 1, E);
-                while (j != i) {
-                    if (step > max_steps) break;
-                    if (fast1 && (uint64_t)st < kPmM) {
-                        // window: lane k screens trial j+k against the lower bound
-                        // lb = corr_nb(ei) + corr_nb(ej) >= c = eah_i + eah_cur(ej)
-                        const int rem = wrap_e(i - j + E, E);
-                        // (ds_bpermute reads 0 from inactive lanes: every lane takes part)
-#if TT_LS_SLP
-                        int pk = j + lane;
-                        if (pk >= E) pk -= E;
-                        if (pk >= E) pk %= E;                      // E < 64 only
-                        const int ej = S.evl[pk], tj = S.slp[pk];
-#else
-                        const int ej = S.evl[wrap_e(j + lane, E)], tj = S.sl[ej];
-#endif
-                        const int xt = bperm(V.x, tj);
-                        bool need = true;
-                        if (lane < rem && tj != t_orig) {
-                            int c1 = 0, c2 = 0, selfj = 0, cij = 0;
-                            for (int w = 0; w < EW; ++w) {
-                                const uint64_t rw = S.pb.corr64[(size_t)ej * EW + w];
-                                c1 += __popcll(rw & S.B[(size_t)tj * EW + w]);
-                                c2 += __popcll(rw & readlane64(bo, w));
-                                if (w == (ej >> 6)) selfj = (int)((rw >> (ej & 63)) & 1ull);
-                                if (w == (ei >> 6)) cij = (int)((rw >> (ei & 63)) & 1ull);
-                            }
-                            const int c = eah_i + S.rp[tj] + c1 - selfj;
-                            int lb = xt - cij + c2;
-                            if (S.sinf) {                          // pair bounds of both touched slots
-                                const uint64_t pej = poss_of(S, ej);
-                                lb += pairs_lb_of(S.sinf[tj], pei, pej, true) + pairs_lb_of(S.sinf[t_orig], pej, pei, true);
-                            }
-                            need = lb < c;
-                        }
-                        bool done;
-                        const int ks = window_resolve(lane, jump, st, step, max_steps, rem, p2, need, done);
-                        if (ks == 64) {
-                            if (done) break;
-                            j = wrap_e(j + 64, E);
-                            continue;
-                        }
-                        j = wrap_e(j + ks, E);
-                    } else {
-                        if (!(pm_next(st) < p2)) { j = wrap_e(j + 1, E); continue; }
-                        step++;
-                    }
-                    // ---- the full trial at j (its draw and step taken)
-                    bool acc = false;
-                    do {
-                        const int ej = S.evl[j];
-                        const int c = eah_i + eah_cur(S, ej);
-                        set_move(S, 2, ei, ej, 0);
-                        build_nb(S);
-                        const int lb = corr_nb(S, ei) + corr_nb(S, ej);    // n >= lb whatever the rooms
-                        LSP_CNT(S, kPfP1m2);
-                        if (lb >= c) break;
-                        if (S.sinf && S.nts == 2 &&
-                            lb + pairs_lb(S, S.ts[0], ej, ei) + pairs_lb(S, S.ts[1], ei, ej) >= c) {
-                            LSP_CNT(S, kPfB2);
-                            break;
-                        }
-                        LSP_CNT(S, kPfP1m2lb);
-                        const TaskRegs tr = load_tasks(S, 7);
-                        if (S.nts == 2) {             // task 0 = slot(ej) plus ei, task 1 = slot(ei) plus ej
-                            if (match_tasks(S, 1, tr)) goto redo;
-                            if (lb + S.misc[0] >= c) { restore_task<0>(S); break; }
-                            if (match_tasks(S, 2, tr)) goto redo;
-                        } else if (match_tasks(S, 7, tr)) goto redo;
-                        const int n = lb + S.misc[task_of(S, slot_nb(S, ei))] + S.misc[task_of(S, slot_nb(S, ej))];
-                        if (n < c) { accept(S);
-                            if (hotm) hot = refresh_hot(S, hot, false); acc = true; break; }
-                        sync_rooms(S, false);
-                    } while (0);
-                    if (acc) { evc = 0; better = true; break; }
-                    j = wrap_e(j + 1, E);
-                }
-                LSP_ADD(S, kPfM2p1, t_m2);
-                if (better) { better = false; continue; }
-            }
-            if (p3 != 0) {
-                for (int j = wrap_e(i + 1, E); j != i; j = wrap_e(j + 1, E)) {
-                    if (step > max_steps) break;
-                    for (int k = wrap_e(j + 1, E); k != i; k = wrap_e(k + 1, E)) {
-                        if (step > max_steps) break;
-                        const int ej = S.evl[j], ek = S.evl[k];
-                        if (pm_next(st) < p3) {
-                            step++;
-                            const int c = eah_i + eah_cur(S, ej) + eah_cur(S, ek);
-                            set_move(S, 3, ei, ej, ek);
-                            if (build_and_match(S)) goto redo;
-                            const int n = eah_nb(S, ei) + eah_nb(S, ej) + eah_nb(S, ek);
-                            if (n < c) { accept(S);
-                            if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
-                            sync_rooms(S, false);
-                        }
-                        if (step > max_steps) break;
-                        if (pm_next(st) < p3) {
-                            step++;
-                            const int c = eah_i + eah_cur(S, ek) + eah_cur(S, ej);
-                            set_move(S, 3, ei, ek, ej);
-                            if (build_and_match(S)) goto redo;
-                            const int n = eah_nb(S, ei) + eah_nb(S, ek) + eah_nb(S, ej);
-                            if (n < c) { accept(S);
-                            if (hotm) hot = refresh_hot(S, hot, false); evc = 0; better = true; break; }
-                            sync_rooms(S, false);
-                        }
-                    }
-                    if (better) break;
-                }
-                if (better) { better = false; continue; }
-            }
-            evc++;
+        if (S.sinf) {
+#define TT_P1 1
+#include "tt_ls_phase1.inc"
+#undef TT_P1
+        } else {
+            S.sinf = nullptr;                    // known null in this copy (accept, matcher)
+#define TT_P1 0
+#include "tt_ls_phase1.inc"
+#undef TT_P1
         }
     }
     LSP_ADD(S, kPfPh1, t_ph);

@@ -105,7 +105,7 @@ for s in $STEPS; do
     gaab) for i in 1 2; do for l in old new; do run ga8k_${l}_$i 300 python -u tools/bench_ga.py $GA8K --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done ;;
     abr5) run ab_r5_syn 400 python -u tools/ab_eval.py syn 262144 r4:13 r5a:13 r4:13 r5a:13 && run ab_r5_med 300 python -u tools/ab_eval.py med 65536 r4:8 r5a:8 ;;
     lsprofc) prof_fresh; for c in comp15 comp10; do run lsprof_ga_$c 400 python -u tools/ls_prof.py --config $c --pop 65536 --children 8192 --from-ga 0.6 --warm-gens 96 --steps 1000; done ;;
-    pmcgac) PMC_LAST=10 pmc pmc_ga_comp15 local_search_kernel python -u tools/bench_ga.py --config comp15 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 10 --cpu-sample 0 ;;
+    pmcgac) for c in comp15 comp10; do PMC_LAST=10 pmc pmc_ga_$c local_search_kernel python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 10 --cpu-sample 0; done ;;
     abr5b) run ab_r5b_syn 400 python -u tools/ab_eval.py syn 262144 r4:13 r5b:13 r4:13 r5b:13 &&
            run ab_r5b_med 300 python -u tools/ab_eval.py med 65536 r4:8 r5b:8 r5b:9 r4:8 r5b:9 &&
            run ab_r5b_lg 300 python -u tools/ab_eval.py lg 65536 r4:8 r5b:9 r4:8 r5b:9 &&
@@ -128,6 +128,9 @@ for s in $STEPS; do
              run ab_prio2_comp01 400 python -u tools/ab_eval.py comp01 65536 r5f:8 pG:8 pH:8 pI:8 r5f:8 pG:8 pH:8 pI:8 ;;
     gap1f) for i in 1 2; do for c in comp15 comp10 comp01; do for l in r5f0 r5f; do run ga8k_${c}_${l}_$i 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done; done ;;
     gap1g) for i in 1 2; do for c in comp15 comp10 comp01; do for l in r5g0 r5g; do run ga8k_${c}_${l}_$i 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done; done ;;
+    gap1h) for i in 1 2; do for c in comp01 comp15; do for l in r5g0 r5g r5h; do run ga8k_${c}_${l}_$i 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done; done ;;
+    abgrid) run ab_grid_med 300 python -u tools/ab_eval.py med 65536 r5g:8 r5g:1032 r5g:7 r5g:9 r5g:8 r5g:1032 r5g:7 r5g:9 &&
+            run ab_grid_lg 300 python -u tools/ab_eval.py lg 65536 r5g:8 r5g:1032 r5g:7 r5g:9 r5g:8 r5g:1032 r5g:7 r5g:9 ;;
     t6abl) run t6_ablate 300 python -u tools/eval_variants.py med 65536 8,24,40,9,25,41 ;;
     gacomps20) run ga_comps 900 python -u tools/ga_comps.py "$OUT/ga_comps.json" ;;
     gatrace15) run ga8k_trace15 400 rocprofv3 --kernel-trace --stats -d "$OUT/ga_trace15" -o run --output-format csv -- python -u tools/bench_ga.py --config comp15 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 20 --cpu-sample 0 ;;
