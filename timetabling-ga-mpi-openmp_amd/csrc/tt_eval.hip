@@ -1527,7 +1527,8 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
     if (P > 0 && (!hcv || !scv || !feasible || !penalty)) { set_error("null output buffer"); return TT_ERR_INVALID; }
     // profiling-only phase switches (results invalid unless noted): eval_tile5: 1 lane
     // phase, 2 wave phase, 4 correlation words, 8 B-bitset atomics, 16 cell-counter
-    // atomics, 32 workspace zeroing, 64 persistent grid (valid results); wide path: 1
+    // atomics, 32 workspace zeroing, 64 persistent grid, 128 one-tile grid (both valid
+    // results); wide path: 1
     // eval_corr build phase, 2 eval_corr corr phase, 4 no eval_corr launch
     const int ablate = variant >> 4;
     variant &= 15;
@@ -1611,11 +1612,16 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
         };
         auto launch = [&](auto kern, size_t bytes, bool two) -> int {
             const int per_cu = occupancy(kern, bytes, two);
-            // one tile per workgroup: later workgroups start as earlier ones finish, so a
-            // CU's two workgroups drift out of step (one's staging under the other's
-            // compute); the persistent grid kept them in lockstep (med -3 %, lg -4 %,
-            // P = 262,144 -8 %). ablate 64: the persistent grid (comparison only).
-            const int grid = (ablate & 64) ? std::min(tiles, std::max(1, per_cu) * p->num_cus) : tiles;
+            // Grid: with the second tile buffer (two), a persistent grid -- a CU's resident
+            // workgroups loop over their tiles with the next one staged by LDS-DMA under
+            // the current one. Until round 4 it lost to one tile per workgroup (med -3 %,
+            // lg -4 %, P = 262,144 -8 %: the co-resident workgroups ran in lockstep, their
+            // stagings together); with the progress-ordered issue priority (TT_T5_PRIO) it
+            // wins (gpurun_out/r05_i/ab_grid_*.log: med 71.8 -> 69.7 us, lg 94.3 -> 92.5).
+            // Without the second buffer there is nothing to overlap: one tile per workgroup.
+            // ablate 64 forces the persistent grid, 128 the one-tile grid (comparisons).
+            const bool persist = (ablate & 64) || (TT_T5_PRIO && two && !(ablate & 128));
+            const int grid = persist ? std::min(tiles, std::max(1, per_cu) * p->num_cus) : tiles;
             hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NW), bytes, st, p->dev, slot, room, P, hcv, scv,
                                feasible, penalty, ablate);
             return TT_OK;

@@ -131,6 +131,11 @@ for s in $STEPS; do
     gap1h) for i in 1 2; do for c in comp01 comp15; do for l in r5g0 r5g r5h; do run ga8k_${c}_${l}_$i 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done; done ;;
     abgrid) run ab_grid_med 300 python -u tools/ab_eval.py med 65536 r5g:8 r5g:1032 r5g:7 r5g:9 r5g:8 r5g:1032 r5g:7 r5g:9 &&
             run ab_grid_lg 300 python -u tools/ab_eval.py lg 65536 r5g:8 r5g:1032 r5g:7 r5g:9 r5g:8 r5g:1032 r5g:7 r5g:9 ;;
+    abgrid2) run ab_grid2_med 300 python -u tools/ab_eval.py med 65536 r5j:8 r5j:2056 r5j:8 r5j:2056 &&
+             run ab_grid2_lg 300 python -u tools/ab_eval.py lg 65536 r5j:8 r5j:2056 r5j:8 r5j:2056 &&
+             run ab_grid2_comp01 300 python -u tools/ab_eval.py comp01 65536 r5j:8 r5j:2056 r5j:8 r5j:2056 &&
+             run ab_grid2_med262k 300 python -u tools/ab_eval.py med 262144 r5j:8 r5j:2056 r5j:8 r5j:2056 &&
+             run ab_grid2_sm 300 python -u tools/ab_eval.py sm 65536 r5j:8 r5j:2056 r5j:8 r5j:2056 ;;
     t6abl) run t6_ablate 300 python -u tools/eval_variants.py med 65536 8,24,40,9,25,41 ;;
     gacomps20) run ga_comps 900 python -u tools/ga_comps.py "$OUT/ga_comps.json" ;;
     gatrace15) run ga8k_trace15 400 rocprofv3 --kernel-trace --stats -d "$OUT/ga_trace15" -o run --output-format csv -- python -u tools/bench_ga.py --config comp15 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 20 --cpu-sample 0 ;;
