@@ -469,7 +469,7 @@ __device__ __forceinline__ uint32_t mad_u16_hi(uint32_t a, uint32_t b, uint32_t 
 // of a CU's two resident workgroups the one further behind wins the arbiter --
 // instead of the older one (round-4 stamps: the older finishes 31.9 us, its
 // neighbour 43.0 us, and the CU's last workgroup runs alone for 15 us). Same
-// box (gpurun_out/r05_e/ab_prio_*.log): med 74.2 -> 71.8 us, lg 96.9 -> 94.1,
+// box (profiles/r05_ab_tile5_prio.jsonl): med 74.2 -> 71.8 us, lg 96.9 -> 94.1,
 // comp01 100.0 -> 100.1; slower decays measured 72.1-73.1 us at med.
 #ifndef TT_T5_PRIO
 #define TT_T5_PRIO 1
@@ -1617,7 +1617,7 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
             // the current one. Until round 4 it lost to one tile per workgroup (med -3 %,
             // lg -4 %, P = 262,144 -8 %: the co-resident workgroups ran in lockstep, their
             // stagings together); with the progress-ordered issue priority (TT_T5_PRIO) it
-            // wins (gpurun_out/r05_i/ab_grid_*.log: med 71.8 -> 69.7 us, lg 94.3 -> 92.5).
+            // wins (profiles/r05_ab_tile5_grid.jsonl: med 71.8 -> 69.7 us, lg 94.3 -> 92.5).
             // Without the second buffer there is nothing to overlap: one tile per workgroup.
             // ablate 64 forces the persistent grid, 128 the one-tile grid (comparisons).
             const bool persist = (ablate & 64) || (TT_T5_PRIO && two && !(ablate & 128));
