@@ -55,6 +55,7 @@ def main():
     jsonl("r05_ab_tile5_prio.jsonl", [G / f"r05_e/ab_prio_{c}.log" for c in ("med", "lg", "comp01")] +
           [G / f"r05_f/ab_prio2_{c}.log" for c in ("med", "lg", "comp01")])
     jsonl("r05_ab_tile5_grid.jsonl", [G / f"r05_i/ab_grid_{c}.log" for c in ("med", "lg")] +
+          [G / f"r05_k/ab_prio3_{c}.log" for c in ("med", "lg", "comp01")] +
           [G / f"r05_j/ab_grid2_{c}.log" for c in ("med", "lg", "comp01", "med262k", "sm")])
     # local search: pair bounds on the GA (P1B builds against P1B=0 builds, same box)
     rows = []
