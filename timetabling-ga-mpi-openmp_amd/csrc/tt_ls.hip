@@ -36,6 +36,10 @@ constexpr int kLsCapSmall = 64;
 #ifdef TT_LS_PROF
 enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfQ1, kPfQ1c, kPfQ1m, kPfQ2, kPfQ2c, kPfQ2m, kPfP1m2, kPfP1m2lb, kPfP1m1m, kPfP1m1a, kPfP1m1k, kPfVis1, kPfM1p1, kPfM2p1, kPfPh1, kPfPh2, kPfVis2, kPfM1p2, kPfM2p2, kPfSkip1, kPfHot1, kPfMaxTotal, kPfB1, kPfB2, kPfBInit, kPfN };
 __device__ unsigned long long g_ls_prof[kPfN];
+// per individual of the first kLsWaveRec (tools/ls_tail.py): start and end of its wave
+// (s_memrealtime, 100 MHz), its shader cycles and its full trials
+constexpr int kLsWaveRec = 65536;
+__device__ unsigned long long g_ls_wave[4 * kLsWaveRec];
 #define LSP_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define LSP_ADD(St, i, v) ((St).prof[i] += __builtin_amdgcn_s_memtime() - (v))
 #define LSP_CNT(St, i) ((St).prof[i] += 1)
@@ -1237,6 +1241,9 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     const int lane = threadIdx.x;
     LSP_T(t_kernel);
 #ifdef TT_LS_PROF
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+#endif
+#ifdef TT_LS_PROF
     uint64_t t_ph = 0;                  // phase timer (assigned, not declared, between the gotos and redo:)
 #endif
     const LsLayout L = ls_layout(E, R, EW, CAP, smS);
@@ -1600,6 +1607,12 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
 #ifdef TT_LS_PROF
     LSP_ADD(S, kPfTotal, t_kernel);
     LSP_CNT(S, kPfWaves);
+    if (lane == 0 && p < kLsWaveRec) {
+        g_ls_wave[4 * p] = rt_start;
+        g_ls_wave[4 * p + 1] = __builtin_amdgcn_s_memrealtime();
+        g_ls_wave[4 * p + 2] = S.prof[kPfTotal];
+        g_ls_wave[4 * p + 3] = S.prof[kPfTrials];
+    }
     if (lane == 0) {
 #pragma unroll
         for (int i = 0; i < kPfN; ++i)
@@ -1687,6 +1700,15 @@ __global__ __launch_bounds__(1024) void order_check_kernel(const int32_t* __rest
 using namespace ttga;
 
 #ifdef TT_LS_PROF
+extern "C" int tt_ls_wave_read(unsigned long long* out, int reset) {
+    TT_HIP(hipDeviceSynchronize());
+    TT_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ls_wave), sizeof(unsigned long long) * 4 * kLsWaveRec));
+    if (reset) {
+        std::vector<unsigned long long> z(4 * kLsWaveRec, 0ull);
+        TT_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ls_wave), z.data(), sizeof(unsigned long long) * 4 * kLsWaveRec));
+    }
+    return kLsWaveRec;
+}
 extern "C" int tt_ls_prof_read(unsigned long long* out, int reset) {
     TT_HIP(hipDeviceSynchronize());
     TT_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ls_prof), sizeof(unsigned long long) * kPfN));
