@@ -137,7 +137,7 @@ for s in $STEPS; do
              run ab_grid2_med262k 300 python -u tools/ab_eval.py med 262144 r5j:8 r5j:2056 r5j:8 r5j:2056 &&
              run ab_grid2_sm 300 python -u tools/ab_eval.py sm 65536 r5j:8 r5j:2056 r5j:8 r5j:2056 ;;
     abprio3) for c in med lg comp01; do run ab_prio3_$c 400 python -u tools/ab_eval.py $c 65536 r5j:8 q1:8 q2:8 q4:8 r5j:8 q1:8 q2:8 q4:8; done ;;
-    lstail) prof_fresh; for c in comp15 comp10 comp01; do run ls_tail_$c 300 python -u tools/ls_tail.py --config $c; done ;;
+    lstail) prof_fresh; for c in comp15 comp10 comp01; do run ls_tail_$c 300 python -u tools/ls_tail.py --config $c --dump "$OUT/ls_tail_$c.npz"; done ;;
     t6abl) run t6_ablate 300 python -u tools/eval_variants.py med 65536 8,24,40,9,25,41 ;;
     gacomps20) run ga_comps 900 python -u tools/ga_comps.py "$OUT/ga_comps.json" ;;
     gatrace15) run ga8k_trace15 400 rocprofv3 --kernel-trace --stats -d "$OUT/ga_trace15" -o run --output-format csv -- python -u tools/bench_ga.py --config comp15 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 20 --cpu-sample 0 ;;

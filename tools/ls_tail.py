@@ -34,6 +34,7 @@ ap.add_argument("--children", type=int, default=8192)
 ap.add_argument("--steps", type=int, default=1000)
 ap.add_argument("--warm-gens", type=int, default=96)
 ap.add_argument("--warm-feasible", type=float, default=0.6)
+ap.add_argument("--dump", default=None, help="npz of per-child durations, trials and features for offline study")
 a = ap.parse_args()
 
 lib = native.load(native.PKG_DIR / "libttga_prof.so")
@@ -52,6 +53,7 @@ dp.ga_breed(isl.pop["slot"], isl.pop["room"], isl.pop["penalty"], isl.rng_child,
             isl.p_cross, isl.p_mut, isl.skip)
 isl._evaluate(c)
 hcv = c["hcv"].cpu().numpy().copy()
+c_slot0, c_room0 = c["slot"].cpu().numpy().copy(), c["room"].cpu().numpy().copy()
 order = dp.lpt_order(c["hcv"], isl.work)
 n = a.children
 buf = np.zeros(4 * 65536, dtype=np.uint64)
@@ -104,4 +106,28 @@ out = {"config": a.config, "children": n, "warm_gens": gens,
                             "index_order": list_schedule(dur, peak) / 100.0},
        "note": "durations in s_memrealtime units (10 ns); list schedules use the measured durations and the "
                "launch's peak concurrency, so they ignore that a wave runs faster when fewer share its SIMD"}
+if a.dump:
+    # per-child features of the children as searched (their slots and rooms before the search)
+    sl = c_slot0.astype(np.int64)
+    rm = c_room0.astype(np.int64)
+    sn, corr, poss = dp.derived()
+    corr = corr.astype(bool)
+    np.fill_diagonal(corr, False)
+    E, R = inst.E, inst.R
+    cell = sl * R + rm
+    n_cell = np.zeros((n, 45 * R), np.int64)
+    np.add.at(n_cell, (np.arange(n)[:, None], cell), 1)
+    room_pairs = (n_cell * (n_cell - 1) // 2).sum(1)
+    n_slot = np.zeros((n, 45), np.int64)
+    np.add.at(n_slot, (np.arange(n)[:, None], sl), 1)
+    overfull = np.maximum(n_slot - R, 0).sum(1)
+    unsuit = (poss[np.arange(E)[None, :], rm] == 0).sum(1)
+    corr_ev = np.zeros((n, E), np.int64)
+    for i in range(n):
+        same = sl[i][:, None] == sl[i][None, :]
+        corr_ev[i] = (same & corr).sum(1)
+    cell_ev = np.take_along_axis(n_cell, cell, 1) - 1
+    ehcv = corr_ev + cell_ev
+    np.savez_compressed(a.dump, dur=dur, trials=trials, hcv=hcv, room_pairs=room_pairs, corr_pairs=corr_ev.sum(1) // 2,
+                        unsuit=unsuit, overfull=overfull, nhot=(ehcv > 0).sum(1), order_pos=pos)
 print(json.dumps(out, indent=1))
