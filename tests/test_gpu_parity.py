@@ -144,7 +144,9 @@ def test_eval_bench_size_properties(orc):
     slot = torch.randint(0, 45, (P, inst.E), dtype=torch.uint8, device="cuda", generator=g)
     room = dp.assign_rooms(slot)
     a = [host(t) for t in dp.eval(slot, room, variant=8)]
-    for v in (v for v in EVAL_VARIANTS if v != 8):
+    # plus eval_tile5's two grids forced: 8 | 64 << 4 persistent (the default with the
+    # second tile buffer), 8 | 128 << 4 one tile per workgroup
+    for v in [v for v in EVAL_VARIANTS if v != 8] + [8 | (64 << 4), 8 | (128 << 4)]:
         b = [host(t) for t in dp.eval(slot, room, variant=v)]
         for x, y in zip(a, b):
             assert np.array_equal(x, y)

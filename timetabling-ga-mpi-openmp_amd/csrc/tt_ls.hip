@@ -63,6 +63,7 @@ __device__ unsigned long long g_ls_wave[4 * kLsWaveRec];
 struct LsLayout {
     size_t sl, rr, nrr, evl, B, NB, rp, hist, misc, task, slp, pos, ps, sm, sinf;
     size_t task_bytes;
+    size_t scratch;      // the task region: kLsTasks tasks, or the summaries' owner table if larger
     int NT;              // events per matcher task (min(E, 256))
     size_t bytes;
 };
@@ -104,6 +105,16 @@ constexpr int kP1bMaxRooms = 16;
 // SlotInfo[45] of the slots, then [3] of the matcher tasks: 384 B per wave, in the
 // phase-2 student-mask region when there is one (the two phases never overlap)
 constexpr size_t kSinfBytes = sizeof(SlotInfo) * (kSlots + 3);
+// A matcher task: ev [NT] u16 and hist [R] u16 (the wave matcher's), then, only
+// where a slot of more than 64 events can reach the lane-serial matcher (NT > 64),
+// its pl [NT] u64, mr [NT], rm [R] and dr [R]. TT_LS_TASK_COMPACT = 0 allocates
+// the serial matcher's arrays in every launch (the round-4 layout's size: 11 NT +
+// 4 R bytes per task, against 2 NT + 2 R; at E >= 64 the first launch's three
+// tasks take 2.3 KB of a wave's LDS instead of 0.5 KB).
+#ifndef TT_LS_TASK_COMPACT
+#define TT_LS_TASK_COMPACT 1
+#endif
+__host__ __device__ inline size_t task_off_pl(int NT, int R) { return (2 * (size_t)NT + 2 * (size_t)R + 7) & ~(size_t)7; }
 // cap: events per matcher task (kLsCapSmall for the first launch, kMaxSlotEvents for the redo launch)
 // S: students with phase-2 masks (0: none)
 __host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap, int S) {
@@ -143,9 +154,13 @@ __host__ __device__ inline LsLayout ls_layout(int E, int R, int EW, int cap, int
     }
     al(4); L.misc = b; b += 4 * 32;
     L.NT = E < cap ? E : cap;
-    size_t tb = 11 * (size_t)L.NT + 1 + 4 * (size_t)R;   // pl, ev, mr, (pad), hist, rm, dr
-    L.task_bytes = (tb + 15) & ~(size_t)15;
-    al(16); L.task = b; b += kLsTasks * L.task_bytes;
+    L.task_bytes = (task_off_pl(L.NT, R) + (L.NT > 64 || !TT_LS_TASK_COMPACT ? 9 * (size_t)L.NT + 2 * (size_t)R : 0) + 15) &
+                   ~(size_t)15;
+    al(16); L.task = b;
+    L.scratch = kLsTasks * L.task_bytes;
+    // the phase-1 summaries' start-up owner table [45][R] u16 shares the task region
+    if (L.sinf && 2 * (size_t)kSlots * R > L.scratch) L.scratch = (2 * (size_t)kSlots * R + 15) & ~(size_t)15;
+    b += L.scratch;
     L.bytes = (b + 15) & ~(size_t)15;
     return L;
 }
@@ -176,7 +191,7 @@ struct LsState {
     uint16_t* hist;
     int32_t* misc;       // [0..2] neighbour room pairs per task, [3] redo flag, [4..6] events per task
     uint8_t* task_base;
-    int task_bytes, NT;
+    int task_bytes, NT, scratch;
     // neighbour description (wave-uniform)
     int nmv, mv_e[3], mv_t[3];
     int nts, ts[3];
@@ -202,11 +217,11 @@ __device__ __forceinline__ SlotInfo* tsi_of(const LsState& S) { return S.sinf + 
 __device__ __forceinline__ LsTask get_task(const LsState& S, int k) {
     uint8_t* tb = S.task_base + (size_t)k * S.task_bytes;
     LsTask T;
-    T.pl = (uint64_t*)tb;
-    T.ev = (uint16_t*)(tb + 8 * (size_t)S.NT);
-    T.mr = tb + 10 * (size_t)S.NT;
-    T.hist = (uint16_t*)(tb + ((11 * (size_t)S.NT + 1) & ~(size_t)1));
-    T.rm = (uint8_t*)(T.hist + S.R);
+    T.ev = (uint16_t*)tb;
+    T.hist = T.ev + S.NT;
+    T.pl = (uint64_t*)(tb + task_off_pl(S.NT, S.R));      // lane-serial matcher only (NT > 64)
+    T.mr = (uint8_t*)(T.pl + S.NT);
+    T.rm = T.mr + S.NT;
     T.dr = T.rm + S.R;
     return T;
 }
@@ -1010,10 +1025,10 @@ struct SinfView {
     const uint16_t* ps;
     const uint64_t* poss;
     uint8_t* task_base;
-    int E, R, EW, task_bytes;
+    int E, R, EW, scratch;
 };
 __device__ __forceinline__ SinfView sinf_view(const LsState& S) {
-    return SinfView{S.sinf, S.B, S.sl, S.rr, S.ps, S.pb.poss, S.task_base, S.E, S.R, S.EW, S.task_bytes};
+    return SinfView{S.sinf, S.B, S.sl, S.rr, S.ps, S.pb.poss, S.task_base, S.E, S.R, S.EW, S.scratch};
 }
 __device__ __forceinline__ uint64_t vposs(const SinfView& V, int e) { return V.ps ? (uint64_t)V.ps[e] : V.poss[e]; }
 
@@ -1084,7 +1099,7 @@ __device__ __forceinline__ int pairs_lb(LsState& S, int s, int out, int a) {
 __device__ __noinline__ void sinf_init_v(SinfView V) {
     const int E = V.E, R = V.R, lane = threadIdx.x & 63;
     const int NC = kSlots * R;
-    if ((size_t)2 * NC > (size_t)kLsTasks * V.task_bytes) {
+    if ((size_t)2 * NC > (size_t)V.scratch) {
         for (int t = 0; t < kSlots; ++t) sinf_build_v(V, t);
         return;
     }
@@ -1259,6 +1274,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     S.misc = (int32_t*)(lds + L.misc);
     S.task_base = lds + L.task;
     S.task_bytes = (int)L.task_bytes;
+    S.scratch = (int)L.scratch;
     S.NT = L.NT;
     S.nmv = 0; S.nts = 0;
     S.c1_valid = 0;

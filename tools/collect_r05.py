@@ -48,6 +48,8 @@ def main():
     # the wide path's record loads: naive compiler loads, then pinned
     jsonl("r05_ab_lanes_records.jsonl", [G / "r05_a/ab_r5_syn.log", G / "r05_a/ab_r5_med.log",
                                           G / "r05_b/ab_r5b_syn.log"])
+    # the wide path with a falling per-wave issue priority (TT_LANES_PRIO, not kept)
+    jsonl("r05_ab_lanes_prio.jsonl", [G / "r05_l/ab_lp_syn.log"])
     # tile6 and the tile5 priority schedules / grid
     jsonl("r05_ab_tile6.jsonl", [G / "r05_b/ab_r5b_med.log", G / "r05_b/ab_r5b_lg.log", G / "r05_b/ab_r5b_comp01.log",
                                  G / "r05_c/t6_ablate.log", G / "r05_d/ab_t5d_med.log", G / "r05_d/ab_t5d_lg.log",
@@ -65,6 +67,12 @@ def main():
         rows += ga_rows(run, pat)
     (P / "r05_ab_ls_pair_bounds_ga.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
     print("r05_ab_ls_pair_bounds_ga.jsonl", len(rows))
+    # compact matcher tasks (tc1) against the round-4 task layout (tc0) and 6 waves per SIMD (w6)
+    jsonl("r05_ab_ls_task_compact.jsonl", [G / f"r05_o/ab_ls_{c}.log" for c in ("comp01_8192", "med_4096", "med_65536", "lg_8192")])
+    rows = ga_rows("r05_n", "ga8k_comp*_tc*.log") + ga_rows("r05_o", "ga8k_comp*.log")
+    (P / "r05_ab_ga_task_compact.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    if (G / "r05_n/occ_probe.log").exists():
+        shutil.copy(G / "r05_n/occ_probe.log", P / "r05_occ_probe.jsonl")
     for src, dst in (("r05_b/ga8k_comp15_check.log", "r05_ga8k_comp15_bitexact.json"),):
         if (G / src).exists():
             (P / dst).write_text(json.dumps(last_json(G / src), indent=1))
