@@ -201,6 +201,39 @@ def test_eight_islands_lg_vs_oracle(orc):
     assert dp.status() == 0
 
 
+def test_islands_on_streams_match_serial_comp01():
+    """Islands multiplexed on one GPU, each on a stream of its own (ttga.islands
+    --islands K, tools/bench_ga.py --islands K) with their generations enqueued
+    back to back so the launches overlap, end bit-identical to the same islands
+    stepped one after another on torch's current stream: 8,192-child generations
+    (LPT dispatch, the small-task + redo local search) with a migration between."""
+    inst = ttga.config_instance("comp01")
+    dp = native.DeviceProblem(inst)
+    W, N, C, gens, seed, steps = 3, 8192, 4096, 4, 42, 200
+    runs = []
+    for streamed in (False, True):
+        isl = [Island(dp, pop_size=N, children=C, max_steps=steps, seed=rank_seed(seed, g),
+                      stream=torch.cuda.Stream() if streamed else None) for g in range(W)]
+        isl[0].initialize()
+        torch.cuda.synchronize()
+        broadcast_population(isl, 1)
+        torch.cuda.synchronize()
+        for gen in range(gens):
+            if gen == 2:
+                torch.cuda.synchronize()
+                ring_migrate(isl, 0, 1)
+                torch.cuda.synchronize()
+            for i in isl:
+                i.step()
+        torch.cuda.synchronize()
+        runs.append([{k: host(i.pop[k]).copy() for k in KEYS} | {"rng": host(i.rng_child).copy(),
+                                                                 "best": i.best_thread()} for i in isl])
+    for g in range(W):
+        for k in runs[0][g]:
+            assert np.array_equal(runs[0][g][k], runs[1][g][k]), (g, k)
+    assert dp.status() == 0
+
+
 def _lines(text):
     """JSON lines with wall-clock fields removed, grouped per procID in order."""
     per, other = {}, []

@@ -141,7 +141,13 @@ class Island(Members):
 
     def __init__(self, dp, pop_size: int = 10, children: int = 1, max_steps: int = 200, seed: int = 1,
                  p_cross: float = 0.8, p_mut: float = 0.5, skip_init_draws: bool = True, device=None,
-                 p1: float = 1.0, p2: float = 1.0, p3: float = 0.0, lpt: bool | None = None):
+                 p1: float = 1.0, p2: float = 1.0, p3: float = 0.0, lpt: bool | None = None, stream=None):
+        """stream: a torch.cuda.Stream of the island's own, or None (torch's current
+        stream). Islands multiplexed on one GPU (ttga.islands --islands K) each take
+        one, so one island's launches fill the SIMD slots another's local-search tail
+        leaves idle; every host read of the island (member, member_meta, best_thread)
+        synchronises its stream first, and a caller that moves data between islands
+        (migration) synchronises the device around it."""
         import torch
         if not (1 <= children <= pop_size):
             raise ValueError("need 1 <= children <= pop_size")
@@ -160,20 +166,47 @@ class Island(Members):
         self.rng_child = torch.from_numpy(stream_seeds(seed, self.N, self.C)).to(dev)
         self.work = dp.ga_work(self.N)
         self.generation = 0
+        self.stream = stream
+        if stream is not None:
+            stream.wait_stream(torch.cuda.current_stream(dev))     # the zero-filled buffers above
+
+    def _on_stream(self):
+        import contextlib
+
+        import torch
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
+    def sync(self):
+        """Wait for the island's stream (no-op without one)."""
+        if self.stream is not None:
+            self.stream.synchronize()
+
+    def member(self, k: int) -> dict:
+        self.sync()
+        return super().member(k)
+
+    def member_meta(self, k: int):
+        self.sync()
+        return super().member_meta(k)
 
     def _evaluate(self, p):
         self.dp.eval(p["slot"], p["room"], out=(p["hcv"], p["scv"], p["feasible"], p["penalty"]))
 
     def initialize(self):
         """ga.cpp:429-434 for every member, then the population is sorted."""
-        p = self.pop
-        self.dp.random_init(self.rng_init, p["slot"], p["room"])
-        self.dp.local_search(p["slot"], p["room"], self.rng_init, self.max_steps, self.p1, self.p2, self.p3)
-        self._evaluate(p)
-        self.dp.ga_replace(p, None, self.work)
+        with self._on_stream():
+            p = self.pop
+            self.dp.random_init(self.rng_init, p["slot"], p["room"])
+            self.dp.local_search(p["slot"], p["room"], self.rng_init, self.max_steps, self.p1, self.p2, self.p3)
+            self._evaluate(p)
+            self.dp.ga_replace(p, None, self.work)
 
     def step(self):
-        """One generation of C children (ga.cpp:543-585)."""
+        """One generation of C children (ga.cpp:543-585), enqueued on the island's stream."""
+        with self._on_stream():
+            self._step()
+
+    def _step(self):
         c = self.child
         self.dp.ga_breed(self.pop["slot"], self.pop["room"], self.pop["penalty"], self.rng_child, c["slot"], c["room"],
                          self.flags, self.p_cross, self.p_mut, self.skip)
@@ -194,6 +227,7 @@ class Island(Members):
         replacement put the current pop[0] in place: child c of the last
         tt_ga_replace (the source position it leaves in its own slot of the
         work buffer, tt_ga_work_source_offset), else thread 0."""
+        self.sync()
         src = self.dp.ga_work_source(self.work, self.N)
         k = self.N - self.C
         return src - k if self.generation > 0 and k <= src < self.N else 0

@@ -237,11 +237,17 @@ def main(argv=None):
     C = max(1, min(C, N))
     K = max(1, ctl.get("islands", 1))
     W = world * K
+    # K > 1: a stream per island, so one island's launches fill the SIMD slots
+    # another's local-search tail leaves idle (the islands are independent
+    # between migrations)
+    streams = [torch.cuda.Stream(device=device) for _ in range(K)] if K > 1 else [None]
     islands = [Island(dp, pop_size=N, children=C, max_steps=max_steps_for(ctl["problem_type"]),
-                      seed=rank_seed(seed, rank * K + k), p1=ctl["p1"], p2=ctl["p2"], p3=ctl["p3"])
+                      seed=rank_seed(seed, rank * K + k), p1=ctl["p1"], p2=ctl["p2"], p3=ctl["p3"],
+                      stream=streams[k])
                for k in range(K)]
     if rank == 0:
         islands[0].initialize()
+    torch.cuda.synchronize()
     broadcast_population(islands, world, backend, use_dist)
     torch.cuda.synchronize()
     t_begin = time.perf_counter()    # beginTry (ga.cpp:476)
@@ -251,11 +257,14 @@ def main(argv=None):
     gens = ctl.get("generations", math.ceil(TOTAL_CHILDREN / C))
     for g in range(gens):
         if (g + 1) % 100 == 50:
+            torch.cuda.synchronize()             # every island's stream, before the copies
             if use_dist:
                 dist.barrier()
             ring_migrate(islands, rank, world, backend, use_dist)
-        for log, isl in zip(logs, islands):
+            torch.cuda.synchronize()             # the migrants in place before the islands go on
+        for isl in islands:                      # enqueued back to back: the islands' streams overlap
             isl.step()
+        for log, isl in zip(logs, islands):
             log.update(isl, isl.best_thread())
     torch.cuda.synchronize()
     vals = [isl.best_value() for isl in islands]

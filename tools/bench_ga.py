@@ -50,6 +50,7 @@ from ttga.ga import Island  # noqa: E402
 
 sys.path.insert(0, str(REPO))
 from bench import host_cores  # noqa: E402  (every core this job may use + the CPU model)
+from ttga.islands import rank_seed  # noqa: E402
 
 import hashlib  # noqa: E402
 
@@ -72,6 +73,9 @@ def parser():
     ap.add_argument("--lpt", choices=["auto", "on", "off"], default="auto",
                     help="longest-expected-first dispatch of the children's local search (Island default: auto)")
     ap.add_argument("--lib", default=None, help="profiling: an A/B build (tools/ab_build.sh) instead of the in-tree library")
+    ap.add_argument("--islands", type=int, default=1,
+                    help="K independent islands of --pop members on this GPU, each on its own stream (ttga.islands "
+                         "--islands K between migrations); children/s over all K")
     return ap
 
 
@@ -79,20 +83,32 @@ def run_ga(a):
     """One island on the in-tree (or --lib) library; returns the JSON record."""
     inst = ttga.config_instance(a.config)
     dp = native.DeviceProblem(inst)
-    isl = Island(dp, pop_size=a.pop, children=a.children, max_steps=a.steps, seed=a.seed,
-                 lpt=None if a.lpt == "auto" else a.lpt == "on")
+    K = max(1, a.islands)
+    # island k's seed as ttga.islands gives it (ga.cpp:412); one island: --seed, no stream of its own
+    seeds = [a.seed] + [rank_seed(a.seed, k) for k in range(1, K)]
+    isls = [Island(dp, pop_size=a.pop, children=a.children, max_steps=a.steps, seed=seeds[k],
+                   lpt=None if a.lpt == "auto" else a.lpt == "on", stream=torch.cuda.Stream() if K > 1 else None)
+            for k in range(K)]
+    isl = isls[0]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    isl.initialize()
+    for i in isls:
+        i.initialize()
     torch.cuda.synchronize()
     init_s = time.perf_counter() - t0
-    isl.step()                                  # warm-up generation
+    for i in isls:
+        i.step()                                # warm-up generation
     torch.cuda.synchronize()
     warm = 1
-    while warm < a.warm_gens and float(isl.pop["feasible"].float().mean().item()) < a.warm_feasible:
-        isl.step()
+
+    def feasible_fraction():
+        torch.cuda.synchronize()
+        return min(float(i.pop["feasible"].float().mean().item()) for i in isls)
+    while warm < a.warm_gens and feasible_fraction() < a.warm_feasible:
+        for i in isls:
+            i.step()
         warm += 1
-    feas_start = float(isl.pop["feasible"].float().mean().item())
+    feas_start = feasible_fraction()
     torch.cuda.synchronize()
     # snapshot of the population and child streams the CPU sample (and its device replay) breed from
     pop_slot, pop_room = isl.pop["slot"].cpu().numpy().copy(), isl.pop["room"].cpu().numpy().copy()
@@ -102,7 +118,8 @@ def run_ga(a):
     t0 = time.perf_counter()
     gens = 0
     while gens < a.gens or time.perf_counter() - t0 < a.min_seconds:
-        isl.step()
+        for i in isls:                          # K > 1: the islands' streams overlap
+            i.step()
         gens += 1
         # the generations are stream-ordered and need no host round trip; the clock is
         # checked against the device every 8 generations (a sync after every one left
@@ -119,10 +136,10 @@ def run_ga(a):
     pop_digest = _h.hexdigest()[:16]
     pf = isl.pop["feasible"].bool()
     out = {"config": a.config, "E": inst.E, "R": inst.R, "F": inst.F, "S": inst.S, "pop": a.pop,
-           "children_per_gen": a.children, "gens": gens, "max_steps": a.steps, "lpt_dispatch": isl.lpt,
+           "children_per_gen": a.children, "islands": K, "gens": gens, "max_steps": a.steps, "lpt_dispatch": isl.lpt,
            "init_seconds": init_s,
            "warm_gens": warm, "feasible_fraction_at_start": feas_start,
-           "pop_digest": pop_digest, "gpu_seconds": gpu_s, "gpu_children_per_s": a.children * gens / gpu_s,
+           "pop_digest": pop_digest, "gpu_seconds": gpu_s, "gpu_children_per_s": K * a.children * gens / gpu_s,
            "best_scv_feasible": int(isl.pop["scv"][pf].min().item()) if bool(pf.any()) else None,
            "best": {"feasible": feas, "scv": scv, "hcv": hcv, "penalty": pen},
            "feasible_fraction": float(isl.pop["feasible"].float().mean().item())}

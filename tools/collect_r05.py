@@ -71,6 +71,14 @@ def main():
     jsonl("r05_ab_ls_task_compact.jsonl", [G / f"r05_o/ab_ls_{c}.log" for c in ("comp01_8192", "med_4096", "med_65536", "lg_8192")])
     rows = ga_rows("r05_n", "ga8k_comp*_tc*.log") + ga_rows("r05_o", "ga8k_comp*.log")
     (P / "r05_ab_ga_task_compact.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    # islands multiplexed on one GPU, each on its own stream (bench_ga --islands K)
+    rows = ga_rows("r05_q", "ga8k_comp*_isl*.log")
+    for r in rows:
+        r["islands"] = int(r["run"].rsplit("isl", 1)[1])
+    (P / "r05_ga8k_islands_streams.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    if (G / "r05_p/occ_sweep.log").exists():
+        shutil.copy(G / "r05_p/occ_sweep.log", P / "r05_occ_sweep.jsonl")
+    jsonl("r05_ab_ls_poss16.jsonl", [G / f"r05_p/ab_ls_{c}.log" for c in ("comp01_8192", "med_65536")])
     if (G / "r05_n/occ_probe.log").exists():
         shutil.copy(G / "r05_n/occ_probe.log", P / "r05_occ_probe.jsonl")
     for src, dst in (("r05_b/ga8k_comp15_check.log", "r05_ga8k_comp15_bitexact.json"),):

@@ -3,11 +3,12 @@
 // holds. Every workgroup spins ~20 us and records its start and end
 // (s_memrealtime); the host reports the most waves alive at once.
 //
-//   hipcc --offload-arch=gfx950 -O3 tools/occ_probe.hip -o tools/occ_probe && tools/occ_probe
+//   hipcc --offload-arch=gfx950 -O3 tools/occ_probe.hip -o tools/occ_probe && tools/occ_probe [sweep]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
+#include <string>
 #include <vector>
 
 template <int SCR_WORDS>
@@ -61,10 +62,14 @@ static void run(const char* name, int lds_bytes) {
                 4 * SCR, lds_bytes, name, peak(r, n), occ, (int)e);
 }
 
-int main() {
+int main(int argc, char** argv) {
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     std::printf("{\"cus\": %d}\n", cus);
+    if (argc > 1 && std::string(argv[1]) == "sweep") {      // LDS bytes per wave against resident waves
+        for (int b = 4096; b <= 12288; b += 256) run<0>("sweep", b);
+        return 0;
+    }
     run<0>("no scratch", 1024);
     run<0>("no scratch, comp01 LDS", 8032);
     run<0>("no scratch, comp15 LDS", 8816);
