@@ -1607,6 +1607,7 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
                 (void)hipGetLastError();    // not sticky: the launch's own error check must not see it
                 return 0;
             }
+            per_cu = std::min(per_cu, lds_resident_limit(bytes));
             c.store(per_cu, std::memory_order_relaxed);
             return per_cu;
         };

@@ -54,6 +54,16 @@ int check_hip(hipError_t e, const char* what);
         if (_rc != TT_OK) return _rc;                        \
     } while (0)
 
+// Workgroups of `lds_bytes` of LDS each that one gfx950 CU actually keeps
+// resident: LDS is allocated in blocks of 1,280 B (160 KB / 128), which
+// hipOccupancyMaxActiveBlocksPerMultiprocessor does not model (it divides
+// 160 KB by the size rounded to 256 B: 20 against the real 18 at 8,032 B).
+// Measured by tools/occ_probe.hip (profiles/r05_occ_sweep.jsonl).
+inline int lds_resident_limit(size_t lds_bytes) {
+    const size_t blocks = (lds_bytes + 1279) / 1280;
+    return blocks == 0 ? 1 << 30 : (int)(128 / blocks);
+}
+
 // Common argument checks for population entry points.
 int check_pop_args(const tt_problem* p, int P, const void* a, const void* b);
 

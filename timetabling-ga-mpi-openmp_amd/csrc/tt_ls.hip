@@ -1749,6 +1749,9 @@ static int ls_mask_occupancy(const tt_problem* p, int cap, K k) {
         (void)hipGetLastError();
         return 0;
     }
+    o0 = std::min(o0, lds_resident_limit(b0));
+    o1 = std::min(o1, lds_resident_limit(b1));
+    if (o1 < 1) return 0;
     return (std::min(o0, 255) << 8) | std::min(o1, 255);
 }
 
@@ -1829,6 +1832,7 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
         (void)hipGetLastError();        // clear it: the redo launch's check below must see only its own error
         per_cu = 1;
     }
+    per_cu = std::min(per_cu, lds_resident_limit(Lf.bytes));
     const int grid = std::min(P, std::max(1, per_cu) * p->num_cus);
     hipLaunchKernelGGL(local_search_redo_kernel, dim3(grid), dim3(64), Lf.bytes, st, p->dev, slot, room, rng,
                        max_steps, p1, p2, p3, rl->list, rl->cap, smf);

@@ -71,8 +71,17 @@ def main():
     jsonl("r05_ab_ls_task_compact.jsonl", [G / f"r05_o/ab_ls_{c}.log" for c in ("comp01_8192", "med_4096", "med_65536", "lg_8192")])
     rows = ga_rows("r05_n", "ga8k_comp*_tc*.log") + ga_rows("r05_o", "ga8k_comp*.log")
     (P / "r05_ab_ga_task_compact.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    # the build after the compact tasks and the stream islands: bench, LS, GA (tests 234 green in the same call)
+    for src, dst in (("bench", "bench"), ("bench_ls", "ls200"), ("bench_ls1000", "ls1000"), ("ga8k", "ga8k"),
+                     ("ga32k", "ga32k")):
+        f = G / "r05_r" / f"{src}.log"
+        if f.exists():
+            (P / f"r05_r_{dst}.json").write_text(json.dumps(last_json(f), indent=1))
+    f = G / "r05_r/prof/run_kernel_stats.csv"
+    if f.exists():
+        shutil.copy(f, P / "r05_r_bench_kernel_stats.csv")
     # islands multiplexed on one GPU, each on its own stream (bench_ga --islands K)
-    rows = ga_rows("r05_q", "ga8k_comp*_isl*.log")
+    rows = ga_rows("r05_q", "ga8k_comp*_isl*.log") + ga_rows("r05_r", "ga8k_comp*_isl*.log")
     for r in rows:
         r["islands"] = int(r["run"].rsplit("isl", 1)[1])
     (P / "r05_ga8k_islands_streams.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
