@@ -147,6 +147,7 @@ for s in $STEPS; do
     occsweep) run occ_sweep 120 tools/occ_probe sweep ;;
     t6abl) run t6_ablate 300 python -u tools/eval_variants.py med 65536 8,24,40,9,25,41 ;;
     gacomps20) run ga_comps 900 python -u tools/ga_comps.py "$OUT/ga_comps.json" ;;
+    gacomps20i2) run ga_comps_isl2 900 python -u tools/ga_comps.py "$OUT/ga_comps_isl2.json" --islands 2 ;;
     gatrace15) run ga8k_trace15 400 rocprofv3 --kernel-trace --stats -d "$OUT/ga_trace15" -o run --output-format csv -- python -u tools/bench_ga.py --config comp15 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 20 --cpu-sample 0 ;;
     selftest) run bench_self2 300 env TTGA_BENCH_BACKEND=gloo python -u bench.py --gpus 2 --steps 20 --warmup 2 --no-pmc --no-cpu ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python -u bench.py --no-pmc --no-cpu --steps 100 ;;
