@@ -107,8 +107,11 @@ def test_eval_wide_vs_oracle(orc, dims):
     rooms[::2] = orc.problem(inst).assign_rooms(slots[::2])
     exp = orc.problem(inst).eval(slots, rooms)
     slots[5, inst.E - 1] = 45                          # invalid gene in the last (partial) chunk: sentinels
-    exp[0][5] = exp[1][5] = exp[3][5] = -1
-    exp[2][5] = 0
+    slots[6, 0] = 255                                  # and at the first event
+    rooms[7, inst.E // 2] = inst.R                     # an invalid room
+    for q in (5, 6, 7):
+        exp[0][q] = exp[1][q] = exp[3][q] = -1
+        exp[2][q] = 0
     for v in (2, 13):
         got = [host(t) for t in dp.eval(dev(slots), dev(rooms), variant=v)]
         for g, e in zip(got, exp):

@@ -48,6 +48,8 @@ def main():
     # the wide path's record loads: naive compiler loads, then pinned
     jsonl("r05_ab_lanes_records.jsonl", [G / "r05_a/ab_r5_syn.log", G / "r05_a/ab_r5_med.log",
                                           G / "r05_b/ab_r5b_syn.log"])
+    # eval_corr's build phase without the per-event gene branch, 24-bit multiplies (not kept)
+    jsonl("r05_ab_corr_build_branchfree.jsonl", [G / "r05_t/ab_cb_syn.log", G / "r05_t/ab_cb_med.log"])
     # the wide path with a falling per-wave issue priority (TT_LANES_PRIO, not kept)
     jsonl("r05_ab_lanes_prio.jsonl", [G / "r05_l/ab_lp_syn.log"])
     # tile6 and the tile5 priority schedules / grid

@@ -138,6 +138,8 @@ for s in $STEPS; do
              run ab_grid2_sm 300 python -u tools/ab_eval.py sm 65536 r5j:8 r5j:2056 r5j:8 r5j:2056 ;;
     abprio3) for c in med lg comp01; do run ab_prio3_$c 400 python -u tools/ab_eval.py $c 65536 r5j:8 q1:8 q2:8 q4:8 r5j:8 q1:8 q2:8 q4:8; done ;;
     lstail) prof_fresh; for c in comp15 comp10 comp01; do run ls_tail_$c 300 python -u tools/ls_tail.py --config $c --dump "$OUT/ls_tail_$c.npz"; done ;;
+    abcb) run ab_cb_syn 400 python -u tools/ab_eval.py syn 262144 base:13 cb:13 base:13 cb:13 &&
+          run ab_cb_med 300 python -u tools/ab_eval.py med 65536 base:8 cb:8 base:8 cb:8 ;;
     ablp) run ab_lp_syn 400 python -u tools/ab_eval.py syn 262144 r5k:13 lp:13 r5k:13 lp:13 ;;
     gaabx) for i in 1 2; do for c in ${GACFGS:-comp15 comp10 comp01}; do for l in $LIBS; do run ga8k_${c}_${l}_$i 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --lib ab_libs/libttga_$l.so; done; done; done ;;
     ablsx) for c in ${LSCFGS:-comp01:8192 med:4096 med:65536 lg:8192}; do run ab_ls_${c%%:*}_${c##*:} 400 python -u tools/ab_ls.py ${c%%:*} ${c##*:} $LIBS; done ;;
