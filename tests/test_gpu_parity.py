@@ -331,6 +331,46 @@ def test_local_search_ordered_dispatch():
             assert np.array_equal(a, b), name
 
 
+def test_local_search_mask_policy_same_results(orc):
+    """The phase-2 student masks are launched or not by an earlier call's
+    phase-2 share of steps (tt_local_search_stats): on med at 8,192
+    individuals (where the masks cost resident waves) the first call on a fresh
+    stream has no share yet and runs without them, the second, after a
+    phase-2-heavy first call, with them; both give the same slots, rooms and RNG
+    states, and a strided sample matches the oracle. The statistics count
+    phase-2 steps only for individuals that reached phase 2."""
+    inst = ttga.config_instance("med")
+    dp = native.DeviceProblem(inst)
+    P = 8192
+    s0 = dev(ttga.random_slots(ttga.population_seeds(321, P), inst.E)[0])
+    r0 = dp.assign_rooms(s0)
+    dp.local_search(s0, r0, dev(ttga.population_seeds(432, P)), 3000)
+    feas = np.flatnonzero(host(dp.eval(s0, r0)[2]))
+    assert len(feas) > 0
+    pick = torch.from_numpy(feas[np.arange(P) % len(feas)]).cuda()     # feasible individuals only: phase 2 heavy
+    s0, r0 = s0[pick].contiguous(), r0[pick].contiguous()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    runs = []
+    with torch.cuda.stream(st):
+        assert dp.local_search_stats(st) == (0, 0)
+        for k in range(2):
+            s, r, g = s0.clone(), r0.clone(), dev(ttga.population_seeds(543, P))
+            dp.local_search(s, r, g, 1000)
+            st.synchronize()
+            runs.append((host(s), host(r), host(g)))
+            ph2, allsteps = dp.local_search_stats(st)
+            assert 0 < ph2 <= allsteps
+            assert ph2 >= 0.5 * allsteps                       # phase-2 heavy: the second call takes the masks
+    for a, b in zip(*runs):
+        assert np.array_equal(a, b)
+    idx = np.arange(0, P, 257)
+    es, er, eg = orc.problem(inst).local_search(host(s0)[idx], host(r0)[idx], ttga.population_seeds(543, P)[idx], 1000)
+    assert np.array_equal(runs[1][0][idx], es) and np.array_equal(runs[1][1][idx], er)
+    assert np.array_equal(runs[1][2][idx], eg)
+    assert dp.status() == 0
+
+
 def test_local_search_crowded_slots_redo(orc):
     """tt_local_search runs a first launch whose matcher tasks hold 64 events per
     slot; an individual whose trial touches a slot with more events is redone

@@ -28,6 +28,12 @@ struct tt_problem {
         void* stream;
         int32_t* list;
         int cap;
+        // phase-2 steps and all steps of the stream's local-search calls: counted
+        // on the device (ph_dev), copied after each call into pinned host memory
+        // (ph_host) that a later call reads without a sync (tt_ls.hip: the
+        // phase-2 student masks' launch policy)
+        unsigned long long* ph_dev = nullptr;
+        volatile unsigned long long* ph_host = nullptr;
     };
     std::vector<LsRedo> ls_redo;
     std::mutex ls_mu;

@@ -90,6 +90,10 @@ struct LsLayout {
 #define TT_LS_SMASK 1
 #endif
 constexpr size_t kSmaskMaxBytes = 4096;
+// phase-2 share of an earlier call's steps above which the masks are worth resident waves
+#ifndef TT_LS_MASK_SHARE
+#define TT_LS_MASK_SHARE 0.5
+#endif
 // TT_LS_P1B: phase-1 room-pair lower bounds (below, SlotInfo) from a summary
 // of a maximum matching of every slot (45 x 20 B per wave + 128 B scratch).
 #ifndef TT_LS_P1B
@@ -1250,7 +1254,8 @@ template <int CAP>
 __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& pb, uint8_t* __restrict__ slot,
                                                              uint8_t* __restrict__ room, int64_t* __restrict__ rng,
                                                              long p, int max_steps, double p1, double p2, double p3,
-                                                             int32_t* __restrict__ redo_list, int redo_cap, int smS) {
+                                                             int32_t* __restrict__ redo_list, int redo_cap, int smS,
+                                                             unsigned long long* __restrict__ ph_steps) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int E = pb.E, R = pb.R, EW = pb.EW64;
     const int lane = threadIdx.x;
@@ -1419,6 +1424,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
         // owner table in place of the room histogram (rooms are distinct per slot now)
         S.phase2 = 1;
         S.sinf = nullptr;
+        if (ph_steps && lane == 0) S.misc[8] = step;                   // phase-1 steps (for the statistics)
         for (int c = lane; c < kSlots * R; c += 64) S.hist[c] = 0xFFFF;
         if (TT_LS_SMASK && smS > 0) {
             S.sm = (uint64_t*)(lds + L.sm);
@@ -1613,6 +1619,10 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     }
     LSP_ADD(S, kPfPh2, t_ph);
     if (guard > guard_max && lane == 0) atomicOr(pb.status, 4);
+    if (ph_steps && lane == 0) {                 // phase-2 steps, all steps (vector atomics, one lane)
+        atomicAdd(&ph_steps[0], (unsigned long long)(S.phase2 ? step - S.misc[8] : 0));
+        atomicAdd(&ph_steps[1], (unsigned long long)step);
+    }
 
     __syncthreads();
     for (int e = lane; e < E; e += 64) {
@@ -1655,10 +1665,10 @@ template <int CAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE))) void local_search_kernel(
     DevProblem pb, uint8_t* __restrict__ slot, uint8_t* __restrict__ room, int64_t* __restrict__ rng, int P,
     int max_steps, double p1, double p2, double p3, int32_t* __restrict__ redo_list, int redo_cap,
-    const int32_t* __restrict__ order, int smS) {
+    const int32_t* __restrict__ order, int smS, unsigned long long* __restrict__ ph_steps) {
     const long p = order ? (long)order[blockIdx.x] : (long)blockIdx.x;   // dispatch order only
     if ((unsigned long)p >= (unsigned long)P) return;
-    ls_one<CAP>(pb, slot, room, rng, p, max_steps, p1, p2, p3, redo_list, redo_cap, smS);
+    ls_one<CAP>(pb, slot, room, rng, p, max_steps, p1, p2, p3, redo_list, redo_cap, smS, ph_steps);
 }
 
 // Redo launch: a grid of resident waves works through the individuals the
@@ -1668,12 +1678,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE)))
 // there is a list to reset: 52 -> a few us per GA generation).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE))) void local_search_redo_kernel(
     DevProblem pb, uint8_t* __restrict__ slot, uint8_t* __restrict__ room, int64_t* __restrict__ rng, int max_steps,
-    double p1, double p2, double p3, int32_t* __restrict__ redo_list, int redo_cap, int smS) {
+    double p1, double p2, double p3, int32_t* __restrict__ redo_list, int redo_cap, int smS,
+    unsigned long long* __restrict__ ph_steps) {
     const int n = min(redo_list[0], redo_cap);
     if (n == 0) return;             // nothing listed: every wave sees 0, no reset needed (no arrival atomics)
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         __syncthreads();
-        ls_one<kMaxSlotEvents>(pb, slot, room, rng, (long)redo_list[2 + i], max_steps, p1, p2, p3, nullptr, 0, smS);
+        ls_one<kMaxSlotEvents>(pb, slot, room, rng, (long)redo_list[2 + i], max_steps, p1, p2, p3, nullptr, 0, smS,
+                               ph_steps);
     }
     __threadfence();
     if (threadIdx.x == 0 && atomicAdd(&redo_list[1], 1) == (int)gridDim.x - 1) {
@@ -1757,9 +1769,15 @@ static int ls_mask_occupancy(const tt_problem* p, int cap, K k) {
 
 // students with phase-2 masks for a launch of P waves: S where the masks cost no
 // resident waves -- the same occupancy with them, or P small enough that every
-// CU holds all its waves at once with them -- else 0 (memoised per problem)
+// CU holds all its waves at once with them -- or where they cost waves but an
+// earlier call on the stream spent at least kLsMaskShare of its steps in phase 2
+// (phase2 / all, -1: unknown); else 0. Measured on the GA at 8,192 children
+// (profiles/r05_ab_ga_ls_masks.jsonl): masks at 18 instead of 20 waves per CU
+// give comp01 (mostly phase 2) +5 %, comp10 -2 % and comp15 (phase 1 only) -4 %.
+// The masks never change a result, only the launch's speed.
+constexpr double kLsMaskShare = TT_LS_MASK_SHARE;
 template <typename K>
-static int ls_mask_students(const tt_problem* p, int cap, K k, int P) {
+static int ls_mask_students(const tt_problem* p, int cap, K k, int P, double share2 = -1.0) {
     std::atomic<int>& memo = const_cast<tt_problem*>(p)->ls_smask[cap == kMaxSlotEvents ? 0 : 1];
     int m = memo.load(std::memory_order_relaxed);
     if (m < 0) memo.store(m = ls_mask_occupancy(p, cap, k), std::memory_order_relaxed);
@@ -1769,11 +1787,24 @@ static int ls_mask_students(const tt_problem* p, int cap, K k, int P) {
 #endif
     const int o0 = m >> 8, o1 = m & 255;
     const long per_cu = ((long)P + p->num_cus - 1) / p->num_cus;
-    return (o1 >= o0 || per_cu <= o1) ? p->dev.S : 0;
+    return (o1 >= o0 || per_cu <= o1 || share2 >= kLsMaskShare) ? p->dev.S : 0;
 }
 
 // entries of a dispatch order checked per pass of order_check_kernel (128 KB of LDS)
 constexpr int kOrderCheckBits = 128 * 1024 * 8;
+
+extern "C" int tt_local_search_stats(const tt_problem* p, void* stream, uint64_t* steps) {
+    if (!p || !steps) { set_error("null argument"); return TT_ERR_INVALID; }
+    tt_problem* mp = const_cast<tt_problem*>(p);
+    std::lock_guard<std::mutex> lock(mp->ls_mu);
+    steps[0] = steps[1] = 0ull;
+    for (auto& r : mp->ls_redo)
+        if (r.stream == stream && r.ph_host) {
+            steps[0] = r.ph_host[0];
+            steps[1] = r.ph_host[1];
+        }
+    return TT_OK;
+}
 
 extern "C" int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P,
                                int max_steps, double p1, double p2, double p3, void* stream) {
@@ -1800,11 +1831,10 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
     }
     if (p->E <= kLsCapSmall) {                      // no slot can exceed the small tasks
         hipLaunchKernelGGL(local_search_kernel<kMaxSlotEvents>, dim3(P), dim3(64), Lf.bytes, st, p->dev, slot, room,
-                           rng, P, max_steps, p1, p2, p3, (int32_t*)nullptr, 0, order, smf);
+                           rng, P, max_steps, p1, p2, p3, (int32_t*)nullptr, 0, order, smf,
+                           (unsigned long long*)nullptr);
         return check_hip(hipGetLastError(), "local_search launch");
     }
-    const int sms = ls_mask_students(p, kLsCapSmall, local_search_kernel<kLsCapSmall>, P);
-    const LsLayout Ls = ls_layout(p->E, p->R, p->dev.EW64, kLsCapSmall, sms);
     tt_problem* mp = const_cast<tt_problem*>(p);
     std::lock_guard<std::mutex> lock(mp->ls_mu);
     // this stream's redo list (grown stream-ordered: the old one may still be read)
@@ -1815,6 +1845,20 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
         mp->ls_redo.push_back({stream, nullptr, 0});
         rl = &mp->ls_redo.back();
     }
+    if (!rl->ph_dev) {                              // the stream's step counters, once
+        void* h = nullptr;
+        TT_HIP(hipHostMalloc(&h, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+        rl->ph_host = (volatile unsigned long long*)h;
+        rl->ph_host[0] = 0ull;
+        rl->ph_host[1] = 0ull;
+        TT_HIP(hipMallocAsync((void**)&rl->ph_dev, 2 * sizeof(unsigned long long), st));
+        TT_HIP(hipMemsetAsync(rl->ph_dev, 0, 2 * sizeof(unsigned long long), st));
+    }
+    // an earlier call's phase-2 share of its steps, as far as its copy has landed (no sync)
+    const unsigned long long ph2 = rl->ph_host[0], pall = rl->ph_host[1];
+    const double share2 = pall > 0 ? (double)ph2 / (double)pall : -1.0;
+    const int sms = ls_mask_students(p, kLsCapSmall, local_search_kernel<kLsCapSmall>, P, share2);
+    const LsLayout Ls = ls_layout(p->E, p->R, p->dev.EW64, kLsCapSmall, sms);
     if (rl->cap < P) {
         if (rl->list) TT_HIP(hipFreeAsync(rl->list, st));
         rl->list = nullptr;
@@ -1824,7 +1868,7 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
         rl->cap = P;
     }
     hipLaunchKernelGGL(local_search_kernel<kLsCapSmall>, dim3(P), dim3(64), Ls.bytes, st, p->dev, slot, room, rng, P,
-                       max_steps, p1, p2, p3, rl->list, rl->cap, order, sms);
+                       max_steps, p1, p2, p3, rl->list, rl->cap, order, sms, rl->ph_dev);
     TT_HIP(hipGetLastError());
     // the redo launch: resident waves only (an empty list costs one short launch)
     int per_cu = 0;
@@ -1835,7 +1879,7 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
     per_cu = std::min(per_cu, lds_resident_limit(Lf.bytes));
     const int grid = std::min(P, std::max(1, per_cu) * p->num_cus);
     hipLaunchKernelGGL(local_search_redo_kernel, dim3(grid), dim3(64), Lf.bytes, st, p->dev, slot, room, rng,
-                       max_steps, p1, p2, p3, rl->list, rl->cap, smf);
+                       max_steps, p1, p2, p3, rl->list, rl->cap, smf, rl->ph_dev);
     const hipError_t he = hipGetLastError();
     if (he != hipSuccess) {
         // the first launch may have listed individuals: leave the list empty
@@ -1843,5 +1887,8 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
         (void)hipMemsetAsync(rl->list, 0, sizeof(int32_t) * 2, st);
         return check_hip(he, "local_search redo launch");
     }
+    // this call's step counts to the host for a later call's mask decision, then zeroed
+    TT_HIP(hipMemcpyAsync((void*)rl->ph_host, rl->ph_dev, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    TT_HIP(hipMemsetAsync(rl->ph_dev, 0, 2 * sizeof(unsigned long long), st));
     return TT_OK;
 }

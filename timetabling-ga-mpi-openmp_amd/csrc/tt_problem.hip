@@ -252,8 +252,13 @@ int tt_problem_destroy(tt_problem* p) {
         (void)hipSetDevice(p->device);
         if (!p->ls_redo.empty()) {                      // redo lists may be in use on their streams
             (void)hipDeviceSynchronize();
-            for (auto& r : p->ls_redo) (void)hipFreeAsync(r.list, nullptr);
+            for (auto& r : p->ls_redo) {
+                (void)hipFreeAsync(r.list, nullptr);
+                if (r.ph_dev) (void)hipFreeAsync(r.ph_dev, nullptr);
+            }
             (void)hipDeviceSynchronize();
+            for (auto& r : p->ls_redo)
+                if (r.ph_host) (void)hipHostFree((void*)r.ph_host);
         }
         rc = check_hip(hipFree(p->dev_block), "tt_problem_destroy");
         (void)hipSetDevice(prev);

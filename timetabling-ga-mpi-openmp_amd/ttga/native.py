@@ -24,6 +24,7 @@ EXPORTS = (
     "tt_eval_variant", "tt_assign_rooms", "tt_random_init", "tt_crossover", "tt_mutation", "tt_local_search",
     "tt_device_status", "tt_last_error", "tt_version", "tt_ga_breed", "tt_ga_work_bytes", "tt_ga_replace",
     "tt_eval_auto_variant", "tt_local_search_ordered", "tt_lpt_order", "tt_ga_work_source_offset",
+    "tt_local_search_stats",
 )
 
 _lib = None
@@ -59,6 +60,7 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.tt_local_search.argtypes = [vp, vp, vp, vp, i32, i32, dbl, dbl, dbl, vp]
     lib.tt_local_search_ordered.argtypes = [vp, vp, vp, vp, i32, i32, dbl, dbl, dbl, vp, vp]
     lib.tt_lpt_order.argtypes = [vp, vp, i32, vp, vp, vp]
+    lib.tt_local_search_stats.argtypes = [vp, vp, vp]
     lib.tt_device_status.argtypes = [vp, vp]
     lib.tt_eval_auto_variant.argtypes = [vp]
     lib.tt_ga_breed.argtypes = [vp, vp, vp, vp, i32, vp, i32, dbl, dbl, i32, vp, vp, vp, vp]
@@ -204,6 +206,16 @@ class DeviceProblem:
                                                           rng.data_ptr(), P, int(max_steps), float(p1), float(p2),
                                                           float(p3), ctypes.c_void_p(order.data_ptr()),
                                                           self._stream(slot)))
+
+    def local_search_stats(self, stream=None):
+        """(phase-2 steps, all steps) of the last tt_local_search call on the
+        stream (torch's current stream by default) whose counts have reached
+        the host; synchronise first for the latest call (diagnostics)."""
+        import torch
+        st = torch.cuda.current_stream(self.device) if stream is None else stream
+        out = (ctypes.c_ulonglong * 2)()
+        _check(self.lib, self.lib.tt_local_search_stats(self.handle, ctypes.c_void_p(st.cuda_stream), out))
+        return int(out[0]), int(out[1])
 
     def lpt_order(self, key, work):
         """tt_lpt_order: indices of key (int32 CUDA) by key descending, ties by

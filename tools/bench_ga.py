@@ -129,6 +129,7 @@ def run_ga(a):
     torch.cuda.synchronize()
     gpu_s = time.perf_counter() - t0
     feas, scv, hcv, pen = isl.member_meta(0)
+    ph2, allsteps = dp.local_search_stats(isl.stream)      # the last generation's children (diagnostics)
     # digest of the final population (slots, rooms, penalties): equal runs, equal digests
     _h = hashlib.sha256()
     for _k in ("slot", "room", "penalty"):
@@ -138,6 +139,7 @@ def run_ga(a):
     out = {"config": a.config, "E": inst.E, "R": inst.R, "F": inst.F, "S": inst.S, "pop": a.pop,
            "children_per_gen": a.children, "islands": K, "gens": gens, "max_steps": a.steps, "lpt_dispatch": isl.lpt,
            "init_seconds": init_s,
+           "ls_phase2_step_share": ph2 / allsteps if allsteps else None,
            "warm_gens": warm, "feasible_fraction_at_start": feas_start,
            "pop_digest": pop_digest, "gpu_seconds": gpu_s, "gpu_children_per_s": K * a.children * gens / gpu_s,
            "best_scv_feasible": int(isl.pop["scv"][pf].min().item()) if bool(pf.any()) else None,

@@ -82,6 +82,14 @@ def main():
     f = G / "r05_r/prof/run_kernel_stats.csv"
     if f.exists():
         shutil.copy(f, P / "r05_r_bench_kernel_stats.csv")
+    # LS occupancy against the phase-2 student masks on the GA (r05_u/v), then the adaptive policy (r05_w)
+    rows = ga_rows("r05_u", "ga8k_comp*.log") + ga_rows("r05_v", "ga8k_comp*.log")
+    (P / "r05_ab_ga_ls_masks.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    jsonl("r05_ab_ls_wpe4.jsonl", [G / "r05_u/ab_ls_comp01_8192.log", G / "r05_u/ab_ls_med_65536.log"])
+    rows = ga_rows("r05_w", "ga8k_comp*.log")
+    for r in rows:
+        r["ls_phase2_step_share"] = last_json(G / (r["run"] + ".log")).get("ls_phase2_step_share")
+    (P / "r05_ab_ga_mask_policy.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
     # islands multiplexed on one GPU, each on its own stream (bench_ga --islands K)
     rows = ga_rows("r05_q", "ga8k_comp*_isl*.log") + ga_rows("r05_r", "ga8k_comp*_isl*.log")
     for r in rows:
