@@ -222,6 +222,23 @@ class Island(Members):
         self.dp.ga_replace(self.pop, c, self.work)
         self.generation += 1
 
+    def snapshot(self) -> "Snapshot":
+        """pop[0]'s (feasible, scv, hcv) and best_thread()'s source position,
+        copied into pinned host memory on the island's stream behind the work
+        enqueued so far; Snapshot.values() waits for that copy only, so the
+        host can log generation g while generation g + 1 runs."""
+        import torch
+        with self._on_stream():
+            off = int(self.dp.lib.tt_ga_work_source_offset(self.N, self.dp.E))
+            p = self.pop
+            meta = torch.stack([p["feasible"][0].to(torch.int32), p["scv"][0], p["hcv"][0],
+                                self.work[off:off + 4].view(torch.int32)[0]])
+            host = torch.empty(4, dtype=torch.int32, pin_memory=True)
+            host.copy_(meta, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        return Snapshot(host, ev, self.generation, self.N - self.C, self.N)
+
     def best_thread(self) -> int:
         """The reference thread (ga.cpp:498, one per child slot) whose
         replacement put the current pop[0] in place: child c of the last
@@ -231,6 +248,21 @@ class Island(Members):
         src = self.dp.ga_work_source(self.work, self.N)
         k = self.N - self.C
         return src - k if self.generation > 0 and k <= src < self.N else 0
+
+
+class Snapshot:
+    """Island.snapshot(): pop[0]'s fields after a generation, landing in
+    pinned host memory behind an event."""
+
+    def __init__(self, host, event, generation: int, k: int, n: int):
+        self.host, self.event, self.generation, self.k, self.n = host, event, generation, k, n
+
+    def values(self):
+        """(feasible, scv, hcv, best thread) once the copy has landed."""
+        self.event.synchronize()
+        f, scv, hcv, src = (int(v) for v in self.host.tolist())
+        thread = src - self.k if self.generation > 0 and self.k <= src < self.n else 0
+        return bool(f), scv, hcv, thread
 
 
 class CostLog:
@@ -267,6 +299,11 @@ class CostLog:
     def update(self, island, thread_id: int = 0):
         feas, scv, hcv, _ = island.member_meta(0)
         return self.offer(feas, scv, hcv, thread_id)
+
+    def update_from(self, snap: "Snapshot"):
+        """update() from a Snapshot taken right after the generation."""
+        feas, scv, hcv, thread = snap.values()
+        return self.offer(feas, scv, hcv, thread)
 
 
 def run_best_line(feasible: bool, total_best: int) -> str:

@@ -255,17 +255,30 @@ def main(argv=None):
     for log, isl in zip(logs, islands):
         log.update(isl, 0)           # ga.cpp:503
     gens = ctl.get("generations", math.ceil(TOTAL_CHILDREN / C))
+    # a generation's log lines are written once the next generation is enqueued:
+    # the host waits for generation g's pop[0] snapshot while g + 1 runs
+    # (same lines, same order; each line's time is taken when its snapshot lands)
+    pending = []
+
+    def flush():
+        for log, snap in pending:
+            log.update_from(snap)
+        pending.clear()
     for g in range(gens):
         if (g + 1) % 100 == 50:
+            flush()
             torch.cuda.synchronize()             # every island's stream, before the copies
             if use_dist:
                 dist.barrier()
             ring_migrate(islands, rank, world, backend, use_dist)
             torch.cuda.synchronize()             # the migrants in place before the islands go on
+        snaps = []
         for isl in islands:                      # enqueued back to back: the islands' streams overlap
             isl.step()
-        for log, isl in zip(logs, islands):
-            log.update(isl, isl.best_thread())
+            snaps.append(isl.snapshot())
+        flush()
+        pending.extend(zip(logs, snaps))
+    flush()
     torch.cuda.synchronize()
     vals = [isl.best_value() for isl in islands]
     gmin = global_min(min(v for _, v in vals), torch.device("cuda", device), world, backend, use_dist)
