@@ -74,14 +74,20 @@ def main():
     rows = ga_rows("r05_n", "ga8k_comp*_tc*.log") + ga_rows("r05_o", "ga8k_comp*.log")
     (P / "r05_ab_ga_task_compact.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
     # the build after the compact tasks and the stream islands: bench, LS, GA (tests 234 green in the same call)
-    for src, dst in (("bench", "bench"), ("bench_ls", "ls200"), ("bench_ls1000", "ls1000"), ("ga8k", "ga8k"),
-                     ("ga32k", "ga32k")):
-        f = G / "r05_r" / f"{src}.log"
-        if f.exists():
-            (P / f"r05_r_{dst}.json").write_text(json.dumps(last_json(f), indent=1))
-    f = G / "r05_r/prof/run_kernel_stats.csv"
-    if f.exists():
-        shutil.copy(f, P / "r05_r_bench_kernel_stats.csv")
+    # r05_x: the final build (the phase-2 mask policy, deferred island logging; 235 GPU tests green)
+    for run in ("r05_r", "r05_x"):
+        for src, dst in (("bench", "bench"), ("bench_ls", "ls200"), ("bench_ls1000", "ls1000"), ("ga8k", "ga8k"),
+                         ("ga32k", "ga32k"), ("bench_syn", "bench_syn")):
+            f = G / run / f"{src}.log"
+            if f.exists():
+                (P / f"{run}_{dst}.json").write_text(json.dumps(last_json(f), indent=1))
+        for src, dst in (("prof", "bench"), ("prof_syn", "bench_syn")):
+            f = G / run / src / "run_kernel_stats.csv"
+            if f.exists():
+                shutil.copy(f, P / f"{run}_{dst}_kernel_stats.csv")
+    for src, dst in (("r05_y/ga_comps.json", "r05_y_ga_comps20.json"), ("r05_y/ga_comps_isl2.json", "r05_y_ga_comps20_islands2.json")):
+        if (G / src).exists():
+            shutil.copy(G / src, P / dst)
     # LS occupancy against the phase-2 student masks on the GA (r05_u/v), then the adaptive policy (r05_w)
     rows = ga_rows("r05_u", "ga8k_comp*.log") + ga_rows("r05_v", "ga8k_comp*.log")
     (P / "r05_ab_ga_ls_masks.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
@@ -91,7 +97,8 @@ def main():
         r["ls_phase2_step_share"] = last_json(G / (r["run"] + ".log")).get("ls_phase2_step_share")
     (P / "r05_ab_ga_mask_policy.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
     # islands multiplexed on one GPU, each on its own stream (bench_ga --islands K)
-    rows = ga_rows("r05_q", "ga8k_comp*_isl*.log") + ga_rows("r05_r", "ga8k_comp*_isl*.log")
+    rows = ga_rows("r05_q", "ga8k_comp*_isl*.log") + ga_rows("r05_r", "ga8k_comp*_isl*.log") + \
+        ga_rows("r05_y", "ga8k_comp*_isl*.log")
     for r in rows:
         r["islands"] = int(r["run"].rsplit("isl", 1)[1])
     (P / "r05_ga8k_islands_streams.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
