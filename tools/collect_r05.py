@@ -96,6 +96,10 @@ def main():
     for r in rows:
         r["ls_phase2_step_share"] = last_json(G / (r["run"] + ".log")).get("ls_phase2_step_share")
     (P / "r05_ab_ga_mask_policy.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    # LS issue priority rising with a wave's steps (TT_LS_PRIO 128 / 64; not kept)
+    rows = ga_rows("r05_pr", "ga8k_comp*.log")
+    (P / "r05_ab_ga_ls_step_prio.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    jsonl("r05_ab_ls_step_prio.jsonl", [G / "r05_pr/ab_ls_comp01_8192.log", G / "r05_pr/ab_ls_med_65536.log"])
     # islands multiplexed on one GPU, each on its own stream (bench_ga --islands K)
     rows = ga_rows("r05_q", "ga8k_comp*_isl*.log") + ga_rows("r05_r", "ga8k_comp*_isl*.log") + \
         ga_rows("r05_y", "ga8k_comp*_isl*.log")
