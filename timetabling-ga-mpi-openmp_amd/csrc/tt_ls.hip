@@ -1845,12 +1845,14 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
         mp->ls_redo.push_back({stream, nullptr, 0});
         rl = &mp->ls_redo.back();
     }
-    if (!rl->ph_dev) {                              // the stream's step counters, once
+    if (!rl->ph_host) {                             // the stream's step counters, once
         void* h = nullptr;
         TT_HIP(hipHostMalloc(&h, 2 * sizeof(unsigned long long), hipHostMallocDefault));
         rl->ph_host = (volatile unsigned long long*)h;
         rl->ph_host[0] = 0ull;
         rl->ph_host[1] = 0ull;
+    }
+    if (!rl->ph_dev) {
         TT_HIP(hipMallocAsync((void**)&rl->ph_dev, 2 * sizeof(unsigned long long), st));
         TT_HIP(hipMemsetAsync(rl->ph_dev, 0, 2 * sizeof(unsigned long long), st));
     }
