@@ -34,7 +34,7 @@ constexpr int kLsCapSmall = 64;
 // Profiling build (-DTT_LS_PROF, `make libttga_prof.so`, tools/ls_prof.py):
 // per-section shader-clock totals of every wave, summed into g_ls_prof.
 #ifdef TT_LS_PROF
-enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfQ1, kPfQ1c, kPfQ1m, kPfQ2, kPfQ2c, kPfQ2m, kPfP1m2, kPfP1m2lb, kPfP1m1m, kPfP1m1a, kPfP1m1k, kPfVis1, kPfM1p1, kPfM2p1, kPfPh1, kPfPh2, kPfVis2, kPfM1p2, kPfM2p2, kPfSkip1, kPfHot1, kPfMaxTotal, kPfB1, kPfB2, kPfBInit, kPfN };
+enum { kPfInit, kPfBuild, kPfMatch, kPfCorr, kPfScv, kPfSync, kPfFeas, kPfTotal, kPfTrials, kPfVisits, kPfWaves, kPfScramble, kPfMatchCalls, kPfMatchEvents, kPfMatchSteps, kPfQ1, kPfQ1c, kPfQ1m, kPfQ2, kPfQ2c, kPfQ2m, kPfP1m2, kPfP1m2lb, kPfP1m1m, kPfP1m1a, kPfP1m1k, kPfVis1, kPfM1p1, kPfM2p1, kPfPh1, kPfPh2, kPfVis2, kPfM1p2, kPfM2p2, kPfSkip1, kPfHot1, kPfMaxTotal, kPfB1, kPfB2, kPfBInit, kPfP1m2r0, kPfP1m2a, kPfN };
 __device__ unsigned long long g_ls_prof[kPfN];
 // per individual of the first kLsWaveRec (tools/ls_tail.py): start and end of its wave
 // (s_memrealtime, 100 MHz), its shader cycles and its full trials

@@ -21,7 +21,7 @@ NAMES = ["init", "build_and_match", "match_task_wave", "corr_in_set", "scv_terms
          "p1_move2_quick", "p1_move2_lb_ok", "p1_move1_matched", "p1_move1_accepted", "p1_move1_kept_task",
          "visit_setup_p1", "move1_loop_p1", "move2_loop_p1", "phase1", "phase2", "visit_setup_p2", "move1_loop_p2",
          "move2_loop_p2", "skip_p1", "hot_flags_p1", "max_total", "p1_move1_bound_rejects",
-         "p1_move2_bound_rejects", "pair_bound_init"]
+         "p1_move2_bound_rejects", "pair_bound_init", "p1_move2_rejected_after_task0", "p1_move2_accepted"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="med")
