@@ -123,3 +123,30 @@ def test_ring_migration_gloo(world, K):
         assert np.array_equal(after[g][N - 1], before[(g - 1) % W][0])    # best of the left neighbour
         assert np.array_equal(after[g][N - 2], before[(g + 1) % W][1])    # 2nd best of the right neighbour
         assert all(np.array_equal(after[g][k], before[g][k]) for k in range(N - 2))
+
+
+class _Landed:
+    """An event whose copy has already landed (Snapshot.values waits on it)."""
+
+    def synchronize(self):
+        pass
+
+
+def test_snapshot_log_values_and_best_thread():
+    """ttga.islands logs a generation from Island.snapshot's pinned copy: the
+    fields come back as (feasible, scv, hcv, thread), the thread being child c
+    of the last replacement when pop[0] came from child slot N - C + c, else 0
+    (also before the first generation); CostLog.update_from writes the same
+    line CostLog.offer would."""
+    from ttga.ga import CostLog, Snapshot
+    N, C = 10, 4
+    k = N - C
+    s = Snapshot(torch.tensor([1, 37, 0, k + 2], dtype=torch.int32), _Landed(), 3, k, N)
+    assert s.values() == (True, 37, 0, 2)
+    assert Snapshot(torch.tensor([0, 5, 9, 1], dtype=torch.int32), _Landed(), 3, k, N).values() == (False, 5, 9, 0)
+    assert Snapshot(torch.tensor([1, 5, 0, k], dtype=torch.int32), _Landed(), 0, k, N).values()[3] == 0
+    out_a, out_b = io.StringIO(), io.StringIO()
+    a, b = CostLog(3, out_a, 0.0), CostLog(3, out_b, 0.0)
+    a.offer(True, 37, 0, 2, t=0.5)
+    b.offer(*s.values(), t=0.5)
+    assert out_a.getvalue() == out_b.getvalue() != ""
