@@ -7,6 +7,10 @@
 #   ls ls1000 ga8k ga32k gatrace lsprof timeprob profderive pmcderive listpmc
 #   stamps replace ablanes pmc1..pmc4 (headline eval) pmcls (phase-2 local search) pmcga (GA children's
 #   local search) pmcwide (syn wide path) abls abeval
+#   round 5: gaabx / ablsx (GA / LS A/B of ab_libs/libttga_$LIBS, configs in GACFGS / LSCFGS),
+#   gaisl (bench_ga --islands $ISLS), isltests, gacomps20 / gacomps20i2 (20-comp tables, 1 / 2
+#   islands), lstail / lsprofc (LS launch tail and section profiles, profiling library),
+#   occprobe / occsweep (tools/occ_probe: resident waves against LDS and scratch)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
