@@ -102,9 +102,12 @@ def main():
     jsonl("r05_ab_ls_step_prio.jsonl", [G / "r05_pr/ab_ls_comp01_8192.log", G / "r05_pr/ab_ls_med_65536.log"])
     # islands multiplexed on one GPU, each on its own stream (bench_ga --islands K)
     rows = ga_rows("r05_q", "ga8k_comp*_isl*.log") + ga_rows("r05_r", "ga8k_comp*_isl*.log") + \
-        ga_rows("r05_y", "ga8k_comp*_isl*.log")
+        ga_rows("r05_y", "ga8k_comp*_isl*.log") + ga_rows("r05_i3", "ga8k_comp*_isl*.log") + \
+        ga_rows("r05_i4q", "ga8k_comp*_isl*.log")
     for r in rows:
         r["islands"] = int(r["run"].rsplit("isl", 1)[1])
+        if r["run"].startswith("r05_i4q/"):
+            r["env"] = "GPU_MAX_HW_QUEUES=8"     # the other runs: HIP's default, 4 hardware queues
     (P / "r05_ga8k_islands_streams.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
     if (G / "r05_p/occ_sweep.log").exists():
         shutil.copy(G / "r05_p/occ_sweep.log", P / "r05_occ_sweep.jsonl")
