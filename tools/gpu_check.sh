@@ -150,6 +150,7 @@ for s in $STEPS; do
     gaisl) for c in ${GACFGS:-comp15 comp10 comp01}; do for k in ${ISLS:-1 2}; do run ga8k_${c}_isl$k 400 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --islands $k; done; done ;;
     isltests) run pytest_isl 600 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 300 --timeout-method thread -k "islands" ;;
     occprobe) run occ_probe 120 tools/occ_probe ;;
+    gaisltrace) for k in 1 2; do run ga8k_trace15_isl$k 400 rocprofv3 --kernel-trace --stats -d "$OUT/ga_trace15_isl$k" -o run --output-format csv -- python -u tools/bench_ga.py --config comp15 --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 20 --cpu-sample 0 --islands $k; done ;;
     occsweep) run occ_sweep 120 tools/occ_probe sweep ;;
     t6abl) run t6_ablate 300 python -u tools/eval_variants.py med 65536 8,24,40,9,25,41 ;;
     gacomps20) run ga_comps 900 python -u tools/ga_comps.py "$OUT/ga_comps.json" ;;
