@@ -143,10 +143,25 @@ DOMINANT = {8: "eval_tile5_kernel", 9: "eval_tile6_kernel", 13: "eval_", 2: "eva
 
 
 def visible_gpus() -> int:
-    """GPUs this process may use, counted without initialising the GPU
-    (torch.cuda.device_count() does not, on this image)."""
-    import torch
-    return torch.cuda.device_count()
+    """GPUs the ranks may use, counted in a short child process: importing
+    torch maps the HIP runtime into a process, and the launcher parent must
+    stay free of it (it only starts and relays the ranks)."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
+def hip_mapped() -> bool:
+    """Whether the HIP runtime library is mapped into this process."""
+    try:
+        with open("/proc/self/maps") as f:
+            return any("libamdhip64" in ln for ln in f)
+    except OSError:
+        return False
 
 
 def launch_ranks(args) -> int:
@@ -165,8 +180,16 @@ def launch_ranks(args) -> int:
     import subprocess
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    launcher = {"pid": os.getpid(), "hip_mapped_before_launch": hip_mapped(), "visible_gpus": gpus}
     proc = subprocess.Popen(cmd, cwd=str(REPO), env=env, stdout=subprocess.PIPE, text=True)
     for ln in proc.stdout:                   # rank 0's line on stdout; anything else to stderr
+        if ln.startswith("{"):
+            try:
+                d = json.loads(ln)
+                d["launcher"] = launcher     # the parent's own record: it never loaded HIP
+                ln = json.dumps(d) + "\n"
+            except json.JSONDecodeError:
+                pass
         (sys.stdout if ln.startswith("{") else sys.stderr).write(ln)
         sys.stdout.flush()
     return proc.wait()
@@ -181,6 +204,45 @@ def rank_share(args, rank: int, world: int):
         start = rank * base + min(rank, extra)
         return p, start, args.global_pop
     return args.pop, rank * args.pop, args.pop * world
+
+
+def verify_shard(inst, slot, room, out, rows: int = 256) -> dict:
+    """Checker, after the timed region: `rows` individuals of this rank's shard,
+    evenly strided over it, re-evaluated by the CPU oracle (oracle/, test
+    infrastructure) and compared field by field with the GPU's outputs."""
+    from oracle_lib import host_threads, oracle, split_rows
+    P = int(slot.shape[0])
+    idx = np.unique(np.linspace(0, max(P - 1, 0), min(P, rows)).round().astype(np.int64))
+    if idx.size == 0:
+        return {"rows_checked": 0, "matches_oracle": True}
+    import torch
+    ti = torch.from_numpy(idx).to(slot.device)
+    s_np, r_np = slot[ti].cpu().numpy(), room[ti].cpu().numpy()
+    got = [o[ti].cpu().numpy() for o in out]
+    exp = split_rows(oracle().problem(inst).eval, (s_np, r_np), threads=max(1, host_threads() // 2))
+    ok = all(np.array_equal(g, e) for g, e in zip(got, exp))
+    return {"rows_checked": int(idx.size), "matches_oracle": bool(ok)}
+
+
+def rank_record(rank: int, dev, kernel_ms: float, wall: float, P: int, first: int, check: dict) -> dict:
+    """What one rank reports to rank 0: the device it bound (index and PCI
+    location, so distinct ranks can be seen to use distinct GPUs), its kernel
+    time, its shard and the oracle check of that shard."""
+    import torch
+    pr = torch.cuda.get_device_properties(dev)
+    return {"rank": rank, "device": int(dev.index), "pci": f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}",
+            "uuid": str(getattr(pr, "uuid", "")), "host": os.uname().nodename, "kernel_ms": kernel_ms, "wall_s": wall,
+            "pop": P, "first": first, **check}
+
+
+def merge_ranks(records: list, backend: str, world: int) -> dict:
+    """Rank 0's summary of every rank's record (all_gather_object)."""
+    records = sorted(records, key=lambda r: r["rank"])
+    locs = {(r["host"], r["pci"]) for r in records}
+    return {"world": world, "backend": backend, "ranks_verified": sum(1 for r in records if r["matches_oracle"]),
+            "rows_checked": sum(r["rows_checked"] for r in records), "distinct_devices": len(locs),
+            "devices": [{k: r[k] for k in ("rank", "device", "pci", "uuid", "kernel_ms", "rows_checked",
+                                           "matches_oracle")} for r in records]}
 
 
 def main():
@@ -232,6 +294,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != world:            # n_gpus is what the process group holds
+            raise SystemExit(f"bench.py: WORLD_SIZE {world} but the process group has {dist.get_world_size()} ranks")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -281,6 +345,14 @@ def main():
 
     if args.pmc_child:
         return
+    ranks = None
+    if use_dist:
+        # every rank checks its own shard against the oracle (outside the timed region) and
+        # reports its device; rank 0 puts the gathered records into the line
+        rec = rank_record(rank, dev, kernel_ms, wall, P, first, verify_shard(inst, slot, room, out))
+        recs = [None] * dist.get_world_size()
+        dist.all_gather_object(recs, rec)
+        ranks = merge_ranks(recs, dist.get_backend(), dist.get_world_size())
     if rank == 0:
         total = global_pop * args.steps
         value = total / wall_max
@@ -376,6 +448,8 @@ def main():
             line["cpu_baseline"] = cpu_baseline(inst, s_np, r_np, gpu_out)
         if use_dist and world == 1:
             line["config"]["process_group"] = f"{backend} at world 1 (TTGA_BENCH_FORCE_DIST)"
+        if ranks is not None:
+            line["ranks"] = ranks
         print(json.dumps(line), flush=True)
     if use_dist:
         dist.destroy_process_group()

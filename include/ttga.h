@@ -130,13 +130,17 @@ int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8_t* room, i
                             double p1, double p2, double p3, const int32_t* order, void* stream);
 
 /* Diagnostics: the step counts of the last tt_local_search call on `stream`
- * whose device-to-host copy has landed (no synchronisation; synchronise the
- * stream first for the latest call): steps[0] = steps taken in phase 2,
- * steps[1] = all steps (0, 0 before any call of more than 64 events per
- * individual on the stream). The library uses the phase-2 share to decide
- * whether the phase-2 student masks are worth resident waves; results never
- * depend on it. */
+ * (waits for that call's counts, not for the whole stream): steps[0] = steps
+ * taken in phase 2, steps[1] = all steps (0, 0 before any call on the stream
+ * of an instance with more than 64 events). Call k on a stream launches the
+ * phase-2 student masks by the phase-2 share of call k - 2 (waiting for that
+ * call's counts if they have not landed), so a launch's shape depends only on
+ * the sequence of calls; results never depend on it. */
 int tt_local_search_stats(const tt_problem* p, void* stream, uint64_t* steps);
+
+/* Diagnostics: students with phase-2 masks in the first launch of the last
+ * tt_local_search call on `stream` (0: no masks; -1: no such call yet). */
+int tt_local_search_masks(const tt_problem* p, void* stream, int32_t* students);
 
 /* A longest-expected-first dispatch order for tt_local_search_ordered:
  * order[0..n-1] = the indices of key[0..n-1] (device i32, e.g. the children's

@@ -39,3 +39,54 @@ def test_global_pop_below_ranks_rejected():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--global-pop", "3"],
                        cwd=REPO, capture_output=True, text=True, timeout=240)
     assert r.returncode != 0 and "--global-pop" in r.stderr
+
+
+def _verify_rank(rank, world, port, q):
+    """One gloo rank of the N > 1 bench path's check: its shard (CPU tensors
+    standing in for device memory) verified against the oracle, the records
+    all-gathered as the bench does and merged on rank 0."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import ttga
+    from oracle_lib import oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    inst = ttga.config_instance("sm")
+    o = oracle().problem(inst)
+    P = 600
+    s, r, _ = o.random_init(ttga.population_seeds(100 + 1000 * rank, P))
+    out = [torch.from_numpy(x.copy()) for x in o.eval(s, r)]
+    if rank == 1:
+        out[1][599] += 1                      # the last row of rank 1's shard is wrong
+    chk = bench.verify_shard(inst, torch.from_numpy(s), torch.from_numpy(r), out)
+    rec = {"rank": rank, "device": 0, "pci": f"0000:{rank:02x}:00", "uuid": "", "host": "h", "kernel_ms": 1.0,
+           "wall_s": 1.0, "pop": P, "first": rank * P, **chk}
+    recs = [None] * world
+    dist.all_gather_object(recs, rec)
+    if rank == 0:
+        q.put(bench.merge_ranks(recs, dist.get_backend(), dist.get_world_size()))
+    dist.destroy_process_group()
+
+
+def test_rank_verification_gloo_world2():
+    """The N > 1 bench line's self-check on two gloo ranks: each rank checks 256
+    strided rows of its shard (first and last row included) against the oracle;
+    rank 0's summary counts the ranks that matched and the distinct devices."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_verify_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    m = q.get(timeout=240)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert m["world"] == 2 and m["backend"] == "gloo" and m["distinct_devices"] == 2
+    assert m["ranks_verified"] == 1 and m["rows_checked"] == 512
+    assert [d["matches_oracle"] for d in m["devices"]] == [True, False]

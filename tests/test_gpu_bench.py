@@ -55,6 +55,7 @@ def test_bench_two_ranks_rehearsal():
     d = _line(r.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_pop"] == 2 * 65536 and d["value"] > 0
     assert "rehearsal" in d["config"] and "cpu_baseline" not in d
+    _assert_ranks(d, 2, "gloo")
 
 
 def test_bench_rccl_process_group_one_gpu():
@@ -67,6 +68,7 @@ def test_bench_rccl_process_group_one_gpu():
     assert r.returncode == 0, r.stderr[-2000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == 1 and d["value"] > 0 and d["config"]["process_group"].startswith("nccl")
+    _assert_ranks(d, 1, "nccl")
 
 
 def test_bench_self_launch_two_ranks():
@@ -79,6 +81,20 @@ def test_bench_self_launch_two_ranks():
     assert r.returncode == 0, r.stderr[-2000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_pop"] == 131072 and d["scaling"] == "weak" and d["value"] > 0
+    _assert_ranks(d, 2, "gloo")
+    # the launcher parent only starts and relays the ranks: no HIP runtime in it
+    assert d["launcher"]["hip_mapped_before_launch"] is False and d["launcher"]["visible_gpus"] >= 1
+
+
+def _assert_ranks(d, world, backend):
+    """Every rank checked a strided sample of its shard against the oracle and
+    reported the device it bound (gloo rehearsal: both ranks share the GPU)."""
+    rk = d["ranks"]
+    assert rk["world"] == world == d["n_gpus"] and rk["backend"] == backend
+    assert rk["ranks_verified"] == world and rk["rows_checked"] >= 256 * world
+    pairs = {(x["rank"], x["device"]) for x in rk["devices"]}
+    assert len(pairs) == world and sorted(r for r, _ in pairs) == list(range(world))
+    assert all(x["matches_oracle"] and x["kernel_ms"] > 0 and x["pci"] for x in rk["devices"])
 
 
 def test_bench_self_launch_global_pop_strong():
@@ -92,3 +108,4 @@ def test_bench_self_launch_global_pop_strong():
     d = _line(r.stdout)
     assert d["n_gpus"] == 2 and d["scaling"] == "strong"
     assert d["config"]["global_pop"] == 65536 and d["config"]["pop_per_gpu"] == 32768
+    _assert_ranks(d, 2, "gloo")

@@ -332,13 +332,14 @@ def test_local_search_ordered_dispatch():
 
 
 def test_local_search_mask_policy_same_results(orc):
-    """The phase-2 student masks are launched or not by an earlier call's
-    phase-2 share of steps (tt_local_search_stats): on med at 8,192
-    individuals (where the masks cost resident waves) the first call on a fresh
-    stream has no share yet and runs without them, the second, after a
-    phase-2-heavy first call, with them; both give the same slots, rooms and RNG
-    states, and a strided sample matches the oracle. The statistics count
-    phase-2 steps only for individuals that reached phase 2."""
+    """The phase-2 student masks of call k on a stream are launched or not by
+    the phase-2 share of call k - 2's steps (tt_local_search_stats), waited for
+    if needed, so the launch shape depends only on the call sequence: on med at
+    8,192 individuals (where the masks cost resident waves) the first two calls
+    on a fresh stream have no share to go by and run without them, the third,
+    after a phase-2-heavy first call, with them; all three give the same slots,
+    rooms and RNG states, and a strided sample matches the oracle. The
+    statistics count phase-2 steps only for individuals that reached phase 2."""
     inst = ttga.config_instance("med")
     dp = native.DeviceProblem(inst)
     P = 8192
@@ -351,23 +352,27 @@ def test_local_search_mask_policy_same_results(orc):
     s0, r0 = s0[pick].contiguous(), r0[pick].contiguous()
     st = torch.cuda.Stream()
     st.wait_stream(torch.cuda.current_stream())
-    runs = []
+    runs, masks = [], []
     with torch.cuda.stream(st):
-        assert dp.local_search_stats(st) == (0, 0)
-        for k in range(2):
+        assert dp.local_search_stats(st) == (0, 0) and dp.local_search_masks(st) == -1
+        for k in range(3):
             s, r, g = s0.clone(), r0.clone(), dev(ttga.population_seeds(543, P))
-            dp.local_search(s, r, g, 1000)
-            st.synchronize()
-            runs.append((host(s), host(r), host(g)))
-            ph2, allsteps = dp.local_search_stats(st)
-            assert 0 < ph2 <= allsteps
-            assert ph2 >= 0.5 * allsteps                       # phase-2 heavy: the second call takes the masks
-    for a, b in zip(*runs):
-        assert np.array_equal(a, b)
+            dp.local_search(s, r, g, 1000)          # no synchronisation between the calls
+            masks.append(dp.local_search_masks(st))
+            runs.append((s, r, g))
+        st.synchronize()
+        ph2, allsteps = dp.local_search_stats(st)
+        assert 0 < ph2 <= allsteps
+        assert ph2 >= 0.5 * allsteps                       # phase-2 heavy: call 3 takes the masks
+    assert masks == [0, 0, inst.S], masks
+    runs = [tuple(host(t) for t in x) for x in runs]
+    for other in runs[1:]:
+        for a, b in zip(runs[0], other):
+            assert np.array_equal(a, b)
     idx = np.arange(0, P, 257)
     es, er, eg = orc.problem(inst).local_search(host(s0)[idx], host(r0)[idx], ttga.population_seeds(543, P)[idx], 1000)
-    assert np.array_equal(runs[1][0][idx], es) and np.array_equal(runs[1][1][idx], er)
-    assert np.array_equal(runs[1][2][idx], eg)
+    assert np.array_equal(runs[2][0][idx], es) and np.array_equal(runs[2][1][idx], er)
+    assert np.array_equal(runs[2][2][idx], eg)
     assert dp.status() == 0
 
 

@@ -29,11 +29,16 @@ struct tt_problem {
         int32_t* list;
         int cap;
         // phase-2 steps and all steps of the stream's local-search calls: counted
-        // on the device (ph_dev), copied after each call into pinned host memory
-        // (ph_host) that a later call reads without a sync (tt_ls.hip: the
-        // phase-2 student masks' launch policy)
+        // on the device (ph_dev), copied after call k into pinned host memory
+        // ph_host[2 (k & 1) ..] with event ev[k & 1] recorded behind the copy;
+        // call k + 2 waits for that event and decides the phase-2 student masks'
+        // launch from those counts (tt_ls.hip), so a launch's shape depends only
+        // on the sequence of calls, never on host/device timing
         unsigned long long* ph_dev = nullptr;
         volatile unsigned long long* ph_host = nullptr;
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        long calls = 0;
+        int sms_last = 0;        // students with masks in the last call's first launch
     };
     std::vector<LsRedo> ls_redo;
     std::mutex ls_mu;

@@ -1793,16 +1793,44 @@ static int ls_mask_students(const tt_problem* p, int cap, K k, int P, double sha
 // entries of a dispatch order checked per pass of order_check_kernel (128 KB of LDS)
 constexpr int kOrderCheckBits = 128 * 1024 * 8;
 
+// the stream's redo record (ls_mu held)
+static tt_problem::LsRedo* find_redo(tt_problem* mp, void* stream) {
+    for (auto& r : mp->ls_redo)
+        if (r.stream == stream) return &r;
+    return nullptr;
+}
+
 extern "C" int tt_local_search_stats(const tt_problem* p, void* stream, uint64_t* steps) {
     if (!p || !steps) { set_error("null argument"); return TT_ERR_INVALID; }
     tt_problem* mp = const_cast<tt_problem*>(p);
-    std::lock_guard<std::mutex> lock(mp->ls_mu);
     steps[0] = steps[1] = 0ull;
-    for (auto& r : mp->ls_redo)
-        if (r.stream == stream && r.ph_host) {
-            steps[0] = r.ph_host[0];
-            steps[1] = r.ph_host[1];
-        }
+    hipEvent_t ev = nullptr;
+    int slot = 0;
+    {
+        std::lock_guard<std::mutex> lock(mp->ls_mu);
+        const tt_problem::LsRedo* r = find_redo(mp, stream);
+        if (!r || r->calls == 0) return TT_OK;
+        slot = (int)((r->calls - 1) & 1);
+        ev = r->ev[slot];
+    }
+    const int rc = use_device(p);
+    if (rc) return rc;
+    if (ev) TT_HIP(hipEventSynchronize(ev));        // the last call's counts have landed
+    std::lock_guard<std::mutex> lock(mp->ls_mu);
+    const tt_problem::LsRedo* r = find_redo(mp, stream);
+    if (r && r->ph_host) {
+        steps[0] = r->ph_host[2 * slot];
+        steps[1] = r->ph_host[2 * slot + 1];
+    }
+    return TT_OK;
+}
+
+extern "C" int tt_local_search_masks(const tt_problem* p, void* stream, int32_t* students) {
+    if (!p || !students) { set_error("null argument"); return TT_ERR_INVALID; }
+    tt_problem* mp = const_cast<tt_problem*>(p);
+    std::lock_guard<std::mutex> lock(mp->ls_mu);
+    const tt_problem::LsRedo* r = find_redo(mp, stream);
+    *students = r && r->calls > 0 ? r->sms_last : -1;
     return TT_OK;
 }
 
@@ -1836,29 +1864,40 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
         return check_hip(hipGetLastError(), "local_search launch");
     }
     tt_problem* mp = const_cast<tt_problem*>(p);
+    // the counts of this stream's call two calls back (k - 2), waited for outside the lock:
+    // the masks' decision is a function of the call sequence alone
+    hipEvent_t wait_ev = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(mp->ls_mu);
+        tt_problem::LsRedo* rl = find_redo(mp, stream);
+        if (rl && rl->calls >= 2) wait_ev = rl->ev[rl->calls & 1];
+    }
+    if (wait_ev) TT_HIP(hipEventSynchronize(wait_ev));
     std::lock_guard<std::mutex> lock(mp->ls_mu);
     // this stream's redo list (grown stream-ordered: the old one may still be read)
-    tt_problem::LsRedo* rl = nullptr;
-    for (auto& r : mp->ls_redo)
-        if (r.stream == stream) rl = &r;
+    tt_problem::LsRedo* rl = find_redo(mp, stream);
     if (!rl) {
         mp->ls_redo.push_back({stream, nullptr, 0});
         rl = &mp->ls_redo.back();
     }
-    if (!rl->ph_host) {                             // the stream's step counters, once
+    if (!rl->ph_host) {                             // the stream's step counters (two calls' worth), once
         void* h = nullptr;
-        TT_HIP(hipHostMalloc(&h, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+        TT_HIP(hipHostMalloc(&h, 4 * sizeof(unsigned long long), hipHostMallocDefault));
         rl->ph_host = (volatile unsigned long long*)h;
-        rl->ph_host[0] = 0ull;
-        rl->ph_host[1] = 0ull;
+        for (int i = 0; i < 4; ++i) rl->ph_host[i] = 0ull;
     }
+    for (hipEvent_t& e : rl->ev)
+        if (!e) TT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (!rl->ph_dev) {
         TT_HIP(hipMallocAsync((void**)&rl->ph_dev, 2 * sizeof(unsigned long long), st));
         TT_HIP(hipMemsetAsync(rl->ph_dev, 0, 2 * sizeof(unsigned long long), st));
     }
-    // an earlier call's phase-2 share of its steps, as far as its copy has landed (no sync)
-    const unsigned long long ph2 = rl->ph_host[0], pall = rl->ph_host[1];
-    const double share2 = pall > 0 ? (double)ph2 / (double)pall : -1.0;
+    const int cslot = (int)(rl->calls & 1);     // this call's counter slot
+    double share2 = -1.0;
+    if (rl->calls >= 2) {                           // call k - 2's copy (its event waited for above)
+        const unsigned long long ph2 = rl->ph_host[2 * cslot], pall = rl->ph_host[2 * cslot + 1];
+        share2 = pall > 0 ? (double)ph2 / (double)pall : -1.0;
+    }
     const int sms = ls_mask_students(p, kLsCapSmall, local_search_kernel<kLsCapSmall>, P, share2);
     const LsLayout Ls = ls_layout(p->E, p->R, p->dev.EW64, kLsCapSmall, sms);
     if (rl->cap < P) {
@@ -1889,8 +1928,12 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
         (void)hipMemsetAsync(rl->list, 0, sizeof(int32_t) * 2, st);
         return check_hip(he, "local_search redo launch");
     }
-    // this call's step counts to the host for a later call's mask decision, then zeroed
-    TT_HIP(hipMemcpyAsync((void*)rl->ph_host, rl->ph_dev, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    // this call's step counts to the host for call k + 2's mask decision, then zeroed
+    TT_HIP(hipMemcpyAsync((void*)(rl->ph_host + 2 * cslot), rl->ph_dev, 2 * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, st));
     TT_HIP(hipMemsetAsync(rl->ph_dev, 0, 2 * sizeof(unsigned long long), st));
+    TT_HIP(hipEventRecord(rl->ev[cslot], st));
+    rl->sms_last = sms;
+    ++rl->calls;
     return TT_OK;
 }

@@ -257,8 +257,11 @@ int tt_problem_destroy(tt_problem* p) {
                 if (r.ph_dev) (void)hipFreeAsync(r.ph_dev, nullptr);
             }
             (void)hipDeviceSynchronize();
-            for (auto& r : p->ls_redo)
+            for (auto& r : p->ls_redo) {
                 if (r.ph_host) (void)hipHostFree((void*)r.ph_host);
+                for (hipEvent_t e : r.ev)
+                    if (e) (void)hipEventDestroy(e);
+            }
         }
         rc = check_hip(hipFree(p->dev_block), "tt_problem_destroy");
         (void)hipSetDevice(prev);

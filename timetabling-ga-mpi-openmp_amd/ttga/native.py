@@ -24,7 +24,7 @@ EXPORTS = (
     "tt_eval_variant", "tt_assign_rooms", "tt_random_init", "tt_crossover", "tt_mutation", "tt_local_search",
     "tt_device_status", "tt_last_error", "tt_version", "tt_ga_breed", "tt_ga_work_bytes", "tt_ga_replace",
     "tt_eval_auto_variant", "tt_local_search_ordered", "tt_lpt_order", "tt_ga_work_source_offset",
-    "tt_local_search_stats",
+    "tt_local_search_stats", "tt_local_search_masks",
 )
 
 _lib = None
@@ -61,6 +61,7 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.tt_local_search_ordered.argtypes = [vp, vp, vp, vp, i32, i32, dbl, dbl, dbl, vp, vp]
     lib.tt_lpt_order.argtypes = [vp, vp, i32, vp, vp, vp]
     lib.tt_local_search_stats.argtypes = [vp, vp, vp]
+    lib.tt_local_search_masks.argtypes = [vp, vp, vp]
     lib.tt_device_status.argtypes = [vp, vp]
     lib.tt_eval_auto_variant.argtypes = [vp]
     lib.tt_ga_breed.argtypes = [vp, vp, vp, vp, i32, vp, i32, dbl, dbl, i32, vp, vp, vp, vp]
@@ -209,13 +210,23 @@ class DeviceProblem:
 
     def local_search_stats(self, stream=None):
         """(phase-2 steps, all steps) of the last tt_local_search call on the
-        stream (torch's current stream by default) whose counts have reached
-        the host; synchronise first for the latest call (diagnostics)."""
+        stream (torch's current stream by default); waits for that call's
+        counts (diagnostics)."""
         import torch
         st = torch.cuda.current_stream(self.device) if stream is None else stream
         out = (ctypes.c_ulonglong * 2)()
         _check(self.lib, self.lib.tt_local_search_stats(self.handle, ctypes.c_void_p(st.cuda_stream), out))
         return int(out[0]), int(out[1])
+
+    def local_search_masks(self, stream=None) -> int:
+        """Students with phase-2 masks in the last tt_local_search call's first
+        launch on the stream (0: none, -1: no call yet; diagnostics)."""
+        import torch
+        st = torch.cuda.current_stream(self.device) if stream is None else stream
+        out = ctypes.c_int32(0)
+        _check(self.lib, self.lib.tt_local_search_masks(self.handle, ctypes.c_void_p(st.cuda_stream),
+                                                        ctypes.byref(out)))
+        return int(out.value)
 
     def lpt_order(self, key, work):
         """tt_lpt_order: indices of key (int32 CUDA) by key descending, ties by
