@@ -113,6 +113,103 @@ def test_island_generations_vs_oracle(sm, N, C, gens, lpt):
     assert np.all(np.diff(pop["penalty"]) >= 0)
 
 
+def oracle_staggered(o, pop, rng_child, C, gens, steps, flush_after=(), parts=2):
+    """The staggered schedule of Island(schedule="staggered", parts=K) on the
+    oracle's GA primitives: the child streams split into K sub-batches as
+    numpy.array_split does; sub-batch h is bred from the population after the
+    replacement of sub-batch h - K, and sub-batch h - K + 1 is replaced right
+    after that breed; the pending sub-batches are replaced at the end, and after
+    every generation listed in flush_after (a host read of the island)."""
+    sizes = [len(x) for x in np.array_split(np.arange(C), parts)]
+    offs = np.cumsum([0] + sizes)
+    rng = [rng_child[offs[j]:offs[j + 1]].copy() for j in range(parts)]
+    pending = []
+    for g in range(gens):
+        for j in range(parts):
+            cs, cr, fl, rng[j] = o.ga_breed(pop["slot"], pop["room"], pop["penalty"], rng[j], sizes[j], 0.8, 0.5, 1)
+            if len(pending) >= parts - 1:
+                pop = o.ga_replace(pop, pending.pop(0))
+            cs, cr, rng[j] = o.local_search(cs, cr, rng[j], steps)
+            h, sc, f, p = o.eval(cs, cr)
+            pending.append(dict(slot=cs, room=cr, hcv=h, scv=sc, feasible=f, penalty=p))
+        if g in flush_after:
+            while pending:
+                pop = o.ga_replace(pop, pending.pop(0))
+    while pending:
+        pop = o.ga_replace(pop, pending.pop(0))
+    return pop, np.concatenate(rng)
+
+
+@pytest.mark.parametrize("N,C,gens,lpt,reads,parts", [(10, 2, 12, False, (), 2), (16, 7, 6, False, (2,), 2),
+                                                      (64, 48, 5, True, (1, 3), 2), (30, 11, 6, False, (3,), 3),
+                                                      (64, 40, 4, True, (), 4)],
+                         ids=["N10C2", "N16C7_read", "N64C48_lpt_reads", "N30C11_3parts", "N64C40_4parts_lpt"])
+def test_island_staggered_vs_oracle(sm, N, C, gens, lpt, reads, parts):
+    """Island(schedule="staggered"): K sub-batches on K streams, each bred from
+    the population K - 1 sub-batches behind; bit-exact against the same
+    dependency order on the oracle's GA primitives, with host reads of the
+    island (which replace the pending sub-batches) after the generations in
+    `reads`, odd C, uneven parts, and LPT dispatch."""
+    inst, dp, o = sm
+    steps, seed = 120, 41
+    isl = Island(dp, pop_size=N, children=C, max_steps=steps, seed=seed, lpt=lpt, schedule="staggered", parts=parts)
+    isl.initialize()
+    for g in range(gens):
+        isl.step()
+        if g in reads:
+            isl.member_meta(0)
+    pop = oracle_population(o, N, seed, steps)
+    pop, rng = oracle_staggered(o, pop, stream_seeds(seed, N, C), C, gens, steps, reads, parts)
+    isl.sync()
+    for k in KEYS:
+        assert np.array_equal(host(isl.pop[k]), pop[k]), k
+    assert np.array_equal(host(isl.rng_child), rng)
+    assert np.all(np.diff(pop["penalty"].astype(np.uint32)) >= 0)
+
+
+def test_island_staggered_comp01_vs_oracle():
+    """The staggered schedule on a comp01-size instance (the GA bench's
+    configs[2] shape): 512 members, 256 children per generation (LPT on), four
+    generations against the oracle, bit-exact; and the snapshots taken after
+    each generation (the islands driver's log source) equal the population as
+    the oracle has it after that generation's half-batch A."""
+    inst = ttga.config_instance("comp01")
+    dp = native.DeviceProblem(inst)
+    o = oracle().problem(inst)
+    N, C, gens, steps, seed = 512, 256, 4, 300, 7
+    isl = Island(dp, pop_size=N, children=C, max_steps=steps, seed=seed, lpt=True, schedule="staggered")
+    isl.initialize()
+    snaps = []
+    for _ in range(gens):
+        isl.step()
+        snaps.append(isl.snapshot())
+    from oracle_lib import split_rows
+    s, r, g = o.random_init(stream_seeds(seed, 0, N))
+    s, r, g = split_rows(o.local_search, (s, r, g), steps)
+    h, sc, f, p = o.eval(s, r)
+    pop = o.ga_replace(dict(slot=s, room=r, hcv=h, scv=sc, feasible=f, penalty=p),
+                       {k: v[:0] for k, v in dict(slot=s, room=r, hcv=h, scv=sc, feasible=f, penalty=p).items()})
+    hA = C // 2
+    rng = [stream_seeds(seed, N, C)[:hA].copy(), stream_seeds(seed, N, C)[hA:].copy()]
+    pending, firsts = None, []
+    for gg in range(gens):
+        for k in (0, 1):
+            cs, cr, fl, rng[k] = o.ga_breed(pop["slot"], pop["room"], pop["penalty"], rng[k], hA, 0.8, 0.5, 1)
+            if pending is not None:
+                pop = o.ga_replace(pop, pending)
+            cs, cr, rng[k] = split_rows(o.local_search, (cs, cr, rng[k]), steps)
+            hh, sc, f, p = o.eval(cs, cr)
+            pending = dict(slot=cs, room=cr, hcv=hh, scv=sc, feasible=f, penalty=p)
+        firsts.append((bool(pop["feasible"][0]), int(pop["scv"][0]), int(pop["hcv"][0])))
+    pop = o.ga_replace(pop, pending)
+    assert [sn.values()[:3] for sn in snaps] == firsts
+    isl.sync()
+    for k in KEYS:
+        assert np.array_equal(host(isl.pop[k]), pop[k]), k
+    assert np.array_equal(host(isl.rng_child), np.concatenate(rng))
+    assert dp.status() == 0
+
+
 def test_islands_cli_end_to_end(tmp_path, sm):
     """python -m ttga.islands on one GPU: Control-style CLI, JSON lines in the
     reference's format, one self-migration (generation 49), and the printed
@@ -180,6 +277,40 @@ def test_native_driver_matches_python_driver(tmp_path, sm):
     assert len(a) > 3 and a == b
     assert "Max number of threads 3" in cc.stdout
     assert "Warning: No output file given, writing to stdout" in cc.stderr
+    assert_validated(inst, tim, cc.stdout)
+
+
+@pytest.mark.parametrize("args", [["-c", "3", "--generations", "120", "--pop", "12", "--stagger"],
+                                  ["-c", "4096", "--generations", "5", "--pop", "4096", "--stagger"],
+                                  ["-c", "7", "--generations", "60", "--pop", "16", "--stagger-parts", "3"]],
+                         ids=["c3_migration", "c4096_lpt", "c7_3parts"])
+def test_native_driver_matches_python_driver_staggered(tmp_path, sm, args):
+    """Both drivers with --stagger (two sub-batches per generation on two
+    streams, each bred one sub-batch behind) and --stagger-parts 3: identical
+    JSON lines apart from wall-clock times, through a migration (generation
+    49: the pending sub-batches are replaced first) and with LPT dispatch per
+    sub-batch; the staggered run differs from the batch one (a different GA
+    schedule)."""
+    inst, dp, o = sm
+    exe = REPO / "timetabling-ga-mpi-openmp_amd" / "ttga-ga"
+    tim = tmp_path / "sm.tim"
+    ttga.write_tim(inst, tim)
+    base = ["-i", str(tim), "-s", "42", "-p", "1", *args]
+    env = dict(__import__("os").environ, PYTHONPATH=str(REPO / "timetabling-ga-mpi-openmp_amd"))
+    py = subprocess.run([sys.executable, "-m", "ttga.islands", *base], capture_output=True, text=True,
+                        timeout=240, env=env, cwd=str(tmp_path))
+    cc = subprocess.run([str(exe), *base], capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    plain = [a for a in base if a != "--stagger"]
+    if "--stagger-parts" in plain:
+        i = plain.index("--stagger-parts")
+        del plain[i:i + 2]
+    bat = subprocess.run([str(exe), *plain], capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    assert py.returncode == 0, py.stderr[-2000:]
+    assert cc.returncode == 0, cc.stderr[-2000:]
+    assert bat.returncode == 0, bat.stderr[-2000:]
+    a, b = _json_lines(py.stdout), _json_lines(cc.stdout)
+    assert len(a) >= 3 and a == b
+    assert a != _json_lines(bat.stdout)
     assert_validated(inst, tim, cc.stdout)
 
 

@@ -10,7 +10,12 @@
 // one-GPU box.
 //
 //   ttga-ga -i instance.tim [-s seed] [-p type] [-c children]
-//           [-p1 x -p2 y -p3 z] [--gpus G] [--islands K] [--pop N] [--generations n] [--rccl]
+//           [-p1 x -p2 y -p3 z] [--gpus G] [--islands K] [--pop N] [--generations n] [--rccl] [--stagger]
+//
+// --stagger / --stagger-parts P: the children of a generation are 2 / P
+// sub-batches on as many streams, sub-batch h bred from the population after
+// the replacement of sub-batch h - P (ttga/ga.py Island, schedule "staggered";
+// same results as the Python driver with the same option).
 //
 // Reference correspondence:
 //  * CLI: `-key value` pairs and messages of Control::Control (Control.cpp:3-137);
@@ -82,6 +87,7 @@ struct Control {
     std::string input, output;
     int gpus = 1, islands = 0, pop = 10, generations = -1;
     bool rccl = false;
+    int stagger = 0;                              // sub-batches of the staggered schedule (0: batch)
 };
 
 // Control::Control (Control.cpp:3-137) plus the --gpus/--pop/--generations extensions.
@@ -92,7 +98,11 @@ Control parse_control(int argc, char** argv) {
         c.rccl = true;
         args.erase(it);
     }
-    for (const char* k : {"--gpus", "--islands", "--pop", "--generations", "--children"}) {
+    if (auto it = std::find(args.begin(), args.end(), "--stagger"); it != args.end()) {
+        c.stagger = 2;
+        args.erase(it);
+    }
+    for (const char* k : {"--gpus", "--islands", "--pop", "--generations", "--children", "--stagger-parts"}) {
         auto it = std::find(args.begin(), args.end(), k);
         if (it != args.end()) {
             if (it + 1 == args.end()) die(std::string("missing value for ") + k);
@@ -101,6 +111,7 @@ Control parse_control(int argc, char** argv) {
             else if (!std::strcmp(k, "--islands")) c.islands = v;
             else if (!std::strcmp(k, "--pop")) c.pop = v;
             else if (!std::strcmp(k, "--generations")) c.generations = v;
+            else if (!std::strcmp(k, "--stagger-parts")) c.stagger = v;
             else c.threads = v;
             args.erase(it, it + 2);
         }
@@ -396,6 +407,17 @@ struct Island {
     uint8_t *send_best = nullptr, *send_second = nullptr, *recv_buf = nullptr;
     size_t migrant_bytes = 0;
     CostState cost;                                   // setCurrentCost state (ga.cpp:163-167)
+    // staggered schedule (ttga.ga.Island schedule "staggered"): part j of the child
+    // rows [off, off + n) on stream hs[j] with its own work buffer; every population
+    // operation (breed or replace) waits for the previous one (ev_op), so sub-batch h
+    // is bred after the replacement of h - parts and h - parts + 1 is replaced after
+    // the breed of h
+    int parts = 1;
+    struct Part { int off = 0, n = 0; hipStream_t s = nullptr; void* work = nullptr; };
+    std::vector<Part> part;
+    hipEvent_t ev_op = nullptr;
+    std::vector<int> pending;                         // parts searched, not yet replaced (breed order)
+    int last_replace = 0;
 
     void setup(const Instance& inst) {
         check_hip(hipSetDevice(device), "hipSetDevice");
@@ -419,10 +441,27 @@ struct Island {
         check_hip(hipMalloc(&send_best, migrant_bytes), "hipMalloc");
         check_hip(hipMalloc(&send_second, migrant_bytes), "hipMalloc");
         check_hip(hipMalloc(&recv_buf, 2 * migrant_bytes), "hipMalloc");
+        if (parts > 1) {
+            check_hip(hipEventCreateWithFlags(&ev_op, hipEventDisableTiming), "hipEventCreate");
+            part.resize(parts);
+            for (int j = 0, off = 0; j < parts; j++) {          // numpy.array_split's sizes
+                const int n = C / parts + (j < C % parts ? 1 : 0);
+                part[j].off = off;
+                part[j].n = n;
+                off += n;
+                if (j == 0) {
+                    part[j].s = st;
+                    part[j].work = work;
+                } else {
+                    check_hip(hipStreamCreateWithFlags(&part[j].s, hipStreamNonBlocking), "hipStreamCreate");
+                    check_hip(hipMalloc(&part[j].work, std::max<size_t>(tt_ga_work_bytes(N, E), 16)), "hipMalloc");
+                }
+            }
+        }
     }
 
-    void evaluate(Pop& p) {
-        check_tt(tt_eval(tp, p.slot, p.room, p.n, p.hcv, p.scv, p.feasible, p.penalty, st), "tt_eval");
+    void evaluate(Pop& p, hipStream_t s = nullptr) {
+        check_tt(tt_eval(tp, p.slot, p.room, p.n, p.hcv, p.scv, p.feasible, p.penalty, s ? s : st), "tt_eval");
     }
 
     // ga.cpp:429-434 for every member, then the population is sorted
@@ -433,58 +472,130 @@ struct Island {
         check_tt(tt_ga_replace(tp, pop.slot, pop.room, pop.hcv, pop.scv, pop.feasible, pop.penalty, N, pop.slot,
                                pop.room, pop.hcv, pop.scv, pop.feasible, pop.penalty, 0, work, st),
                  "tt_ga_replace");
+        if (parts > 1) check_hip(hipEventRecord(ev_op, st), "hipEventRecord");
+    }
+
+    // children rows [off, off + n) as a population view
+    Pop child_rows(int off, int n) const {
+        Pop v;
+        v.n = n; v.E = E;
+        v.slot = child.slot + (size_t)off * E; v.room = child.room + (size_t)off * E;
+        v.feasible = child.feasible + off; v.hcv = child.hcv + off; v.scv = child.scv + off;
+        v.penalty = child.penalty + off;
+        return v;
+    }
+
+    // breed n children into rows [off, off + n) on stream s
+    void breed(int off, int n, hipStream_t s) {
+        Pop c = child_rows(off, n);
+        check_tt(tt_ga_breed(tp, pop.slot, pop.room, pop.penalty, N, rng_child + off, n, p_cross, p_mut, 1, c.slot,
+                             c.room, flags + off, s),
+                 "tt_ga_breed");
+    }
+
+    // LPT order (C >= kLptMinChildren), localSearch and evaluation of rows [off, off + n) on s
+    void search(int off, int n, hipStream_t s, void* w) {
+        Pop c = child_rows(off, n);
+        if (order) {
+            // longest-expected first: the children's hcv before the search, descending
+            // (a generation's search launch ends with its slowest children); same results
+            evaluate(c, s);
+            check_tt(tt_lpt_order(tp, c.hcv, n, order + off, w, s), "tt_lpt_order");
+            check_tt(tt_local_search_ordered(tp, c.slot, c.room, rng_child + off, n, max_steps, p1, p2, p3, order + off,
+                                             s),
+                     "tt_local_search_ordered");
+        } else {
+            check_tt(tt_local_search(tp, c.slot, c.room, rng_child + off, n, max_steps, p1, p2, p3, s),
+                     "tt_local_search");
+        }
+        evaluate(c, s);
+    }
+
+    void replace(int off, int n, hipStream_t s, void* w) {
+        Pop c = child_rows(off, n);
+        check_tt(tt_ga_replace(tp, pop.slot, pop.room, pop.hcv, pop.scv, pop.feasible, pop.penalty, N, c.slot, c.room,
+                               c.hcv, c.scv, c.feasible, c.penalty, n, w, s),
+                 "tt_ga_replace");
     }
 
     // one generation of C children (ga.cpp:543-585)
     void step() {
-        check_tt(tt_ga_breed(tp, pop.slot, pop.room, pop.penalty, N, rng_child, C, p_cross, p_mut, 1, child.slot,
-                             child.room, flags, st),
-                 "tt_ga_breed");
-        if (order) {
-            // longest-expected first: the children's hcv before the search, descending
-            // (a generation's search launch ends with its slowest children); same results
-            evaluate(child);
-            check_tt(tt_lpt_order(tp, child.hcv, C, order, work, st), "tt_lpt_order");
-            check_tt(tt_local_search_ordered(tp, child.slot, child.room, rng_child, C, max_steps, p1, p2, p3, order, st),
-                     "tt_local_search_ordered");
-        } else {
-            check_tt(tt_local_search(tp, child.slot, child.room, rng_child, C, max_steps, p1, p2, p3, st),
-                     "tt_local_search");
+        if (parts > 1) {
+            for (int j = 0; j < parts; j++) part_step(j);
+            return;
         }
-        evaluate(child);
-        check_tt(tt_ga_replace(tp, pop.slot, pop.room, pop.hcv, pop.scv, pop.feasible, pop.penalty, N, child.slot,
-                               child.room, child.hcv, child.scv, child.feasible, child.penalty, C, work, st),
-                 "tt_ga_replace");
+        breed(0, C, st);
+        search(0, C, st, work);
+        replace(0, C, st, work);
     }
 
-    Member member(int k) {
+    void part_step(int j) {
+        const Part& p = part[j];
+        check_hip(hipStreamWaitEvent(p.s, ev_op, 0), "hipStreamWaitEvent");      // breed(h) after replace(h - parts)
+        breed(p.off, p.n, p.s);
+        check_hip(hipEventRecord(ev_op, p.s), "hipEventRecord");
+        if ((int)pending.size() >= parts - 1) replace_oldest();                 // replace(h - parts + 1) after breed(h)
+        search(p.off, p.n, p.s, p.work);
+        pending.push_back(j);
+    }
+
+    void replace_oldest() {
+        const int j = pending.front();
+        pending.erase(pending.begin());
+        const Part& p = part[j];
+        check_hip(hipStreamWaitEvent(p.s, ev_op, 0), "hipStreamWaitEvent");
+        replace(p.off, p.n, p.s, p.work);
+        check_hip(hipEventRecord(ev_op, p.s), "hipEventRecord");
+        last_replace = j;
+    }
+
+    // staggered: replace the pending sub-batches; st then follows the population's last operation
+    void flush() {
+        if (parts <= 1) return;
+        while (!pending.empty()) replace_oldest();
+        check_hip(hipStreamWaitEvent(st, ev_op, 0), "hipStreamWaitEvent");
+    }
+
+    // pop[k]'s fields, read behind the last replacement enqueued (staggered: the
+    // pending half-batch stays pending, as ttga.ga.Island.snapshot)
+    Member member_now(int k) {
+        const hipStream_t s = parts > 1 ? part[last_replace].s : st;
         Member m{};
         uint8_t f = 0;
-        check_hip(hipMemcpyAsync(&f, pop.feasible + k, 1, hipMemcpyDeviceToHost, st), "hipMemcpy");
-        check_hip(hipMemcpyAsync(&m.scv, pop.scv + k, 4, hipMemcpyDeviceToHost, st), "hipMemcpy");
-        check_hip(hipMemcpyAsync(&m.hcv, pop.hcv + k, 4, hipMemcpyDeviceToHost, st), "hipMemcpy");
-        check_hip(hipMemcpyAsync(&m.penalty, pop.penalty + k, 4, hipMemcpyDeviceToHost, st), "hipMemcpy");
-        check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+        check_hip(hipMemcpyAsync(&f, pop.feasible + k, 1, hipMemcpyDeviceToHost, s), "hipMemcpy");
+        check_hip(hipMemcpyAsync(&m.scv, pop.scv + k, 4, hipMemcpyDeviceToHost, s), "hipMemcpy");
+        check_hip(hipMemcpyAsync(&m.hcv, pop.hcv + k, 4, hipMemcpyDeviceToHost, s), "hipMemcpy");
+        check_hip(hipMemcpyAsync(&m.penalty, pop.penalty + k, 4, hipMemcpyDeviceToHost, s), "hipMemcpy");
+        check_hip(hipStreamSynchronize(s), "hipStreamSynchronize");
         m.feasible = f != 0;
         return m;
     }
 
-    // the reference thread whose replacement put pop[0] in place (ga.cpp:580-585):
-    // child c of the last tt_ga_replace (the source position it leaves at
-    // tt_ga_work_source_offset in `work`), else 0
-    int best_thread(bool after_step) {
-        if (!after_step) return 0;
-        int32_t s = 0;
-        check_hip(hipMemcpyAsync(&s, (const uint8_t*)work + tt_ga_work_source_offset(N, E), 4, hipMemcpyDeviceToHost,
-                                 st), "hipMemcpy");
-        check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
-        const long src = s, k = N - C;
-        return src >= k && src < N ? (int)(src - k) : 0;
+    // pop[k]'s fields with every half-batch replaced
+    Member member(int k) {
+        flush();
+        return member_now(k);
     }
 
-    // setCurrentCost (ga.cpp:203-228) on pop[0]
+    // the reference thread whose replacement put pop[0] in place (ga.cpp:580-585):
+    // child c of the last tt_ga_replace (the source position it leaves at
+    // tt_ga_work_source_offset in its work buffer), else 0
+    int best_thread(bool after_step) {
+        if (!after_step) return 0;
+        const hipStream_t s = parts > 1 ? part[last_replace].s : st;
+        const void* w = parts > 1 ? part[last_replace].work : work;
+        const int base = parts > 1 ? part[last_replace].off : 0, nb = parts > 1 ? part[last_replace].n : C;
+        int32_t src = 0;
+        check_hip(hipMemcpyAsync(&src, (const uint8_t*)w + tt_ga_work_source_offset(N, E), 4, hipMemcpyDeviceToHost, s),
+                  "hipMemcpy");
+        check_hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+        const long k = N - nb;
+        return src >= k && src < N ? (int)(base + src - k) : 0;
+    }
+
+    // setCurrentCost (ga.cpp:203-228) on pop[0] as the last replacement left it
     void log_cost(Output& out, std::chrono::steady_clock::time_point t0, int thread) {
-        const Member m = member(0);
+        const Member m = member_now(0);
         long entry = 0;
         if (cost.offer(m.feasible, m.scv, m.hcv, entry)) out.line(log_line(entry, id, thread, seconds_since(t0)));
     }
@@ -513,6 +624,7 @@ struct Island {
         cp(pop.scv + pos, buf + 2 * E + 4, 4);
         cp(pop.penalty + pos, buf + 2 * E + 8, 4);
         cp(pop.feasible + pos, buf + 2 * E + 12, 1);
+        if (parts > 1) check_hip(hipEventRecord(ev_op, st), "hipEventRecord");   // the next breed sees the migrants
     }
 
     void release() {
@@ -521,6 +633,11 @@ struct Island {
         for (void* p : {(void*)rng_init, (void*)rng_child, (void*)flags, work, (void*)order, (void*)send_best,
                         (void*)send_second, (void*)recv_buf})
             if (p) (void)hipFree(p);
+        for (size_t j = 1; j < part.size(); j++) {
+            if (part[j].work) (void)hipFree(part[j].work);
+            if (part[j].s) (void)hipStreamDestroy(part[j].s);
+        }
+        if (ev_op) (void)hipEventDestroy(ev_op);
         if (st) (void)hipStreamDestroy(st);
         if (tp) tt_problem_destroy(tp);
     }
@@ -571,6 +688,7 @@ int main(int argc, char** argv) {
         I.max_steps = max_steps_for(ctl.problem_type);
         I.seed = island_seed(ctl.seed, k);
         I.p1 = ctl.p1; I.p2 = ctl.p2; I.p3 = ctl.p3;
+        I.parts = ctl.stagger >= 2 ? std::min(ctl.stagger, C) : 1;
     }
     std::vector<ncclComm_t> comms(K, nullptr);
     if (rccl) {
@@ -612,6 +730,7 @@ int main(int argc, char** argv) {
             cp(I.pop.penalty, z.penalty, 4 * (size_t)N);
             cp(I.pop.feasible, z.feasible, (size_t)N);
         }
+        if (I.parts > 1) check_hip(hipEventRecord(I.ev_op, I.st), "hipEventRecord");   // the shared population
         sync(I);
         barrier.wait();
         if (k == 0) t_begin = std::chrono::steady_clock::now();      // beginTry (ga.cpp:476)
@@ -620,6 +739,7 @@ int main(int argc, char** argv) {
         const int right = (k + 1) % K, left = (k + K - 1) % K;
         for (int g = 0; g < gens; g++) {
             if ((g + 1) % 100 == 50) {   // ga.cpp:514-540, one migrant each way
+                I.flush();                                // staggered: the pending sub-batches replaced first
                 I.pack(0, I.send_best);                   // best, then 2nd best (N >= 3: untouched by dir 0)
                 I.pack(1, I.send_second);
                 sync(I);

@@ -137,11 +137,29 @@ class Members:
 
 
 class Island(Members):
-    """One island: population [N] + C child slots, all device-resident."""
+    """One island: population [N] + C child slots, all device-resident.
+
+    schedule "batch": a generation breeds all C children from the population,
+    searches them in one launch and replaces the C worst (the next generation
+    waits for the slowest child). schedule "staggered": the child slots are
+    split into `parts` sub-batches (part j: child slots [j*C/parts, ...) rounded
+    as numpy.array_split) on as many streams, and sub-batch h is bred from the
+    population after the replacement of sub-batch h - parts, so sub-batch h's
+    local search runs while the searches of h - parts + 1 .. h - 1 finish. The
+    population operations are totally ordered -- breed(h) after replace(h -
+    parts), replace(h - parts + 1) after breed(h) -- so results are
+    deterministic, and C children are in flight at every breed, as in the batch
+    schedule and as with ga.cpp:488-588's C threads breeding from the shared
+    population while the other threads' children are still searched. step()
+    advances `parts` sub-batches and leaves parts - 1 of them pending; flush()
+    replaces them (every host read of the population flushes first; the
+    snapshots the drivers log from do not).
+    """
 
     def __init__(self, dp, pop_size: int = 10, children: int = 1, max_steps: int = 200, seed: int = 1,
                  p_cross: float = 0.8, p_mut: float = 0.5, skip_init_draws: bool = True, device=None,
-                 p1: float = 1.0, p2: float = 1.0, p3: float = 0.0, lpt: bool | None = None, stream=None):
+                 p1: float = 1.0, p2: float = 1.0, p3: float = 0.0, lpt: bool | None = None, stream=None,
+                 schedule: str = "batch", parts: int = 2):
         """stream: a torch.cuda.Stream of the island's own, or None (torch's current
         stream). Islands multiplexed on one GPU (ttga.islands --islands K) each take
         one, so one island's launches fill the SIMD slots another's local-search tail
@@ -151,6 +169,10 @@ class Island(Members):
         import torch
         if not (1 <= children <= pop_size):
             raise ValueError("need 1 <= children <= pop_size")
+        if schedule not in ("batch", "staggered"):
+            raise ValueError("schedule must be 'batch' or 'staggered'")
+        if schedule == "staggered" and not (2 <= parts <= children):
+            raise ValueError("the staggered schedule needs 2 <= parts <= children")
         dev = torch.device("cuda", dp.device if device is None else device)
         super().__init__(new_population(int(pop_size), dp.E, dev))
         self.dp, self.C = dp, int(children)
@@ -167,19 +189,70 @@ class Island(Members):
         self.work = dp.ga_work(self.N)
         self.generation = 0
         self.stream = stream
+        self.schedule = schedule
+        self.parts = int(parts) if schedule == "staggered" else 1
+        self._snap = None
+        self._streams = [stream]
+        if schedule == "staggered":
+            bounds = np.cumsum([0] + [len(x) for x in np.array_split(np.arange(self.C), self.parts)])
+            # sub-batch j: its child rows, child streams, flags and work buffer; part 0 runs
+            # on the island's stream, the others on streams of their own
+            self._part = [{"off": int(bounds[j]), "rows": slice(int(bounds[j]), int(bounds[j + 1])),
+                           "work": self.work if j == 0 else dp.ga_work(self.N)} for j in range(self.parts)]
+            for d in self._part:
+                r = d["rows"]
+                d.update(child={k: v[r] for k, v in self.child.items()}, rng=self.rng_child[r], flags=self.flags[r])
+            self._streams = [stream] + [torch.cuda.Stream(dev) for _ in range(self.parts - 1)]
+            self._ev_op = torch.cuda.Event()          # the last population operation (breed or replace)
+            self._pending = []                        # parts searched but not yet replaced, in breed order
+            self._last_replace = 0                    # part whose work buffer holds the last replace's source
         if stream is not None:
             stream.wait_stream(torch.cuda.current_stream(dev))     # the zero-filled buffers above
+        for st in self._streams[1:]:
+            st.wait_stream(torch.cuda.current_stream(dev) if stream is None else stream)
+        # the buffers were allocated on the creating stream and are used on the island's
+        # own stream(s): tell the caching allocator, so a dropped island's blocks are not
+        # handed out again while its kernels may still write them
+        self._side_streams = [st for st in self._streams if st is not None]
+        self._record_streams(self._owned())
 
-    def _on_stream(self):
+    def _owned(self):
+        ts = list(self.pop.values()) + list(self.child.values()) + [self.flags, self.rng_init, self.rng_child,
+                                                                    self.work]
+        if self.schedule == "staggered":
+            ts += [d["work"] for d in self._part[1:]]
+        return ts
+
+    def _record_streams(self, tensors):
+        for st in self._side_streams:
+            for t in tensors:
+                t.record_stream(st)
+
+    def close(self):
+        """Wait for everything the island has enqueued (its buffers can then be
+        freed safely whatever the allocator knows)."""
+        import torch
+        self.flush()
+        for st in self._side_streams:
+            st.synchronize()
+        torch.cuda.current_stream(self.pop["slot"].device).synchronize()
+
+    def _on_stream(self, stream=None):
         import contextlib
 
         import torch
-        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+        st = self.stream if stream is None else stream
+        return torch.cuda.stream(st) if st is not None else contextlib.nullcontext()
 
     def sync(self):
-        """Wait for the island's stream (no-op without one)."""
+        """Wait for the island's work: pending sub-batches are replaced first
+        (staggered schedule), then the island's stream is waited for."""
+        import torch
+        self.flush()
         if self.stream is not None:
             self.stream.synchronize()
+        elif self.schedule == "staggered":
+            torch.cuda.current_stream(self.pop["slot"].device).synchronize()
 
     def member(self, k: int) -> dict:
         self.sync()
@@ -200,69 +273,156 @@ class Island(Members):
             self.dp.local_search(p["slot"], p["room"], self.rng_init, self.max_steps, self.p1, self.p2, self.p3)
             self._evaluate(p)
             self.dp.ga_replace(p, None, self.work)
+            if self.schedule == "staggered":
+                self._ev_op.record()
 
     def step(self):
-        """One generation of C children (ga.cpp:543-585), enqueued on the island's stream."""
+        """One generation of C children (ga.cpp:543-585), enqueued on the island's
+        stream(s): the whole batch, or (staggered) each sub-batch in turn."""
+        if self.schedule == "staggered":
+            for j in range(self.parts):
+                self._part_step(j)
+            self.generation += 1
+            return
         with self._on_stream():
             self._step()
 
-    def _step(self):
-        c = self.child
-        self.dp.ga_breed(self.pop["slot"], self.pop["room"], self.pop["penalty"], self.rng_child, c["slot"], c["room"],
-                         self.flags, self.p_cross, self.p_mut, self.skip)
+    def _search(self, c, rng, work):
+        """LPT order (optional), localSearch and evaluation of children c."""
         order = None
         if self.lpt:
             # dispatch the children longest-expected first (hcv before the search,
             # descending): the launch's tail is its slowest waves; results unchanged
             self._evaluate(c)
-            order = self.dp.lpt_order(c["hcv"], self.work)
-        self.dp.local_search(c["slot"], c["room"], self.rng_child, self.max_steps, self.p1, self.p2, self.p3,
-                             order=order)
+            order = self.dp.lpt_order(c["hcv"], work)
+        self.dp.local_search(c["slot"], c["room"], rng, self.max_steps, self.p1, self.p2, self.p3, order=order)
         self._evaluate(c)
+
+    def _step(self):
+        c = self.child
+        self.dp.ga_breed(self.pop["slot"], self.pop["room"], self.pop["penalty"], self.rng_child, c["slot"], c["room"],
+                         self.flags, self.p_cross, self.p_mut, self.skip)
+        self._search(c, self.rng_child, self.work)
         self.dp.ga_replace(self.pop, c, self.work)
         self.generation += 1
 
+    def _part_step(self, j: int):
+        """Sub-batch j: bred from the population behind the last population
+        operation; then, with parts - 1 sub-batches pending, the oldest of them
+        is replaced behind that breed; then sub-batch j is searched."""
+        import torch
+        d, st = self._part[j], self._streams[j]
+        with self._on_stream(st):
+            torch.cuda.current_stream().wait_event(self._ev_op)           # breed(h) after replace(h - parts)
+            self.dp.ga_breed(self.pop["slot"], self.pop["room"], self.pop["penalty"], d["rng"], d["child"]["slot"],
+                             d["child"]["room"], d["flags"], self.p_cross, self.p_mut, self.skip)
+            self._ev_op.record()
+        if len(self._pending) >= self.parts - 1:
+            self._replace_oldest()                                          # replace(h - parts + 1) after breed(h)
+        with self._on_stream(st):
+            self._search(d["child"], d["rng"], d["work"])
+        self._pending.append(j)
+
+    def _replace_oldest(self):
+        import torch
+        j = self._pending.pop(0)
+        d = self._part[j]
+        with self._on_stream(self._streams[j]):
+            torch.cuda.current_stream().wait_event(self._ev_op)
+            self.dp.ga_replace(self.pop, d["child"], d["work"])
+            self._ev_op.record()
+        self._last_replace = j
+
+    def flush(self):
+        """Staggered schedule: replace the pending sub-batches in order, and make
+        the island's stream wait for the population's last operation (no-op for
+        the batch schedule)."""
+        import torch
+        if self.schedule != "staggered":
+            return
+        while self._pending:
+            self._replace_oldest()
+        with self._on_stream():
+            torch.cuda.current_stream().wait_event(self._ev_op)
+
+    def _work_of_last_replace(self):
+        return self._part[self._last_replace]["work"] if self.schedule == "staggered" else self.work
+
     def snapshot(self) -> "Snapshot":
         """pop[0]'s (feasible, scv, hcv) and best_thread()'s source position,
-        copied into pinned host memory on the island's stream behind the work
-        enqueued so far; Snapshot.values() waits for that copy only, so the
-        host can log generation g while generation g + 1 runs."""
+        copied into pinned host memory behind the last replacement enqueued
+        (staggered: pending sub-batches stay pending, so the snapshot is the
+        population as the last replacement left it); Snapshot.values() waits for
+        that copy only, so the host can log generation g while generation g + 1
+        runs. Two pinned buffers and events are reused in turn (generation g's
+        snapshot is read after g + 1 has been enqueued)."""
         import torch
-        with self._on_stream():
+        if self._snap is None:
+            self._snap = [(torch.empty(4, dtype=torch.int32, pin_memory=True), torch.cuda.Event()) for _ in range(2)]
+            self._snap_meta = torch.empty(4, dtype=torch.int32, device=self.pop["slot"].device)
+            self._record_streams([self._snap_meta])
+            self._snap_i = 0
+            self._snap_owner = [None, None]
+        i = self._snap_i
+        host, ev = self._snap[i]
+        if self._snap_owner[i] is not None:
+            self._snap_owner[i].values()     # the buffer's previous snapshot, read before the reuse
+        self._snap_i ^= 1
+        st = self._streams[self._last_replace] if self.schedule == "staggered" else None
+        with self._on_stream(st):
             off = int(self.dp.lib.tt_ga_work_source_offset(self.N, self.dp.E))
-            p = self.pop
-            meta = torch.stack([p["feasible"][0].to(torch.int32), p["scv"][0], p["hcv"][0],
-                                self.work[off:off + 4].view(torch.int32)[0]])
-            host = torch.empty(4, dtype=torch.int32, pin_memory=True)
-            host.copy_(meta, non_blocking=True)
-            ev = torch.cuda.Event()
+            p, w = self.pop, self._work_of_last_replace()
+            m = self._snap_meta
+            m[0] = p["feasible"][0]
+            m[1] = p["scv"][0]
+            m[2] = p["hcv"][0]
+            m[3] = w[off:off + 4].view(torch.int32)[0]
+            host.copy_(m, non_blocking=True)
             ev.record()
-        return Snapshot(host, ev, self.generation, self.N - self.C, self.N)
+        snap = Snapshot(host, ev, self.generation, self.N - self._last_batch(), self.N, self._thread_base())
+        self._snap_owner[i] = snap
+        return snap
+
+    def _last_batch(self) -> int:
+        """Children merged by the last replacement (best_thread's offset)."""
+        if self.schedule != "staggered":
+            return self.C
+        return self._part[self._last_replace]["child"]["slot"].shape[0]
+
+    def _thread_base(self) -> int:
+        """Child slot of the last replacement's first child (staggered: its part's offset)."""
+        return self._part[self._last_replace]["off"] if self.schedule == "staggered" else 0
 
     def best_thread(self) -> int:
         """The reference thread (ga.cpp:498, one per child slot) whose
         replacement put the current pop[0] in place: child c of the last
         tt_ga_replace (the source position it leaves in its own slot of the
-        work buffer, tt_ga_work_source_offset), else thread 0."""
+        work buffer, tt_ga_work_source_offset), else thread 0. Staggered: the
+        child slot index over all sub-batches, after the pending ones are
+        replaced."""
         self.sync()
-        src = self.dp.ga_work_source(self.work, self.N)
-        k = self.N - self.C
-        return src - k if self.generation > 0 and k <= src < self.N else 0
+        src = self.dp.ga_work_source(self._work_of_last_replace(), self.N)
+        k = self.N - self._last_batch()
+        return self._thread_base() + src - k if self.generation > 0 and k <= src < self.N else 0
 
 
 class Snapshot:
     """Island.snapshot(): pop[0]'s fields after a generation, landing in
     pinned host memory behind an event."""
 
-    def __init__(self, host, event, generation: int, k: int, n: int):
-        self.host, self.event, self.generation, self.k, self.n = host, event, generation, k, n
+    def __init__(self, host, event, generation: int, k: int, n: int, base: int = 0):
+        self.host, self.event, self.generation, self.k, self.n, self.base = host, event, generation, k, n, base
+        self._vals = None
 
     def values(self):
-        """(feasible, scv, hcv, best thread) once the copy has landed."""
-        self.event.synchronize()
-        f, scv, hcv, src = (int(v) for v in self.host.tolist())
-        thread = src - self.k if self.generation > 0 and self.k <= src < self.n else 0
-        return bool(f), scv, hcv, thread
+        """(feasible, scv, hcv, best thread) once the copy has landed (read once:
+        the pinned buffer is reused two snapshots later)."""
+        if self._vals is None:
+            self.event.synchronize()
+            f, scv, hcv, src = (int(v) for v in self.host.tolist())
+            thread = self.base + src - self.k if self.generation > 0 and self.k <= src < self.n else 0
+            self._vals = (bool(f), scv, hcv, thread)
+        return self._vals
 
 
 class CostLog:

@@ -12,6 +12,9 @@ Reference correspondence:
   ga.cpp (every JSON line goes to stdout, ga.cpp:60). `-c` (threads) sets the
   children bred per generation. Extensions: `--pop N` (ga.cpp:64 has 10,
   N >= 3), `--islands K` (islands per process, default 1), `--generations G`,
+  `--stagger` / `--stagger-parts P` (the children of a generation as 2 / P
+  sub-batches on as many streams, each bred P - 1 sub-batches behind:
+  ttga.ga.Island's staggered schedule),
   `--backend nccl|gloo` (gloo stages migrants through host memory; with it
   several ranks may share one GPU), `--force-dist` (initialise the process
   group and route the broadcast, the ring send/recv pairs and the MIN through
@@ -48,10 +51,13 @@ def parse_control(argv, out=sys.stdout, err=sys.stderr) -> dict:
     """Control::Control (Control.cpp:3-137): `-key value` pairs."""
     args = list(argv)
     extra = {}
-    for k in ("--pop", "--children", "--generations", "--islands"):
+    if "--stagger" in args:               # the staggered schedule (ttga.ga.Island), 2 sub-batches
+        args.remove("--stagger")
+        extra["stagger"] = 2
+    for k in ("--pop", "--children", "--generations", "--islands", "--stagger-parts"):
         if k in args:
             i = args.index(k)
-            extra[k[2:]] = int(args[i + 1])
+            extra[k[2:].replace("-", "_")] = int(args[i + 1])
             del args[i:i + 2]
     if len(args) % 2 != 0:
         err.write("Parse error: Number of command line parameters incorrect\nUsage:\n" + USAGE + "\n")
@@ -241,9 +247,11 @@ def main(argv=None):
     # another's local-search tail leaves idle (the islands are independent
     # between migrations)
     streams = [torch.cuda.Stream(device=device) for _ in range(K)] if K > 1 else [None]
+    # the staggered schedule: --stagger (2 sub-batches) or --stagger-parts P, at most C
+    parts = min(C, ctl.get("stagger_parts", ctl.get("stagger", 0)))
     islands = [Island(dp, pop_size=N, children=C, max_steps=max_steps_for(ctl["problem_type"]),
                       seed=rank_seed(seed, rank * K + k), p1=ctl["p1"], p2=ctl["p2"], p3=ctl["p3"],
-                      stream=streams[k])
+                      stream=streams[k], schedule="staggered" if parts >= 2 else "batch", parts=max(parts, 2))
                for k in range(K)]
     if rank == 0:
         islands[0].initialize()
@@ -267,6 +275,8 @@ def main(argv=None):
     for g in range(gens):
         if (g + 1) % 100 == 50:
             flush()
+            for isl in islands:                  # staggered: the pending half-batch replaced first
+                isl.flush()
             torch.cuda.synchronize()             # every island's stream, before the copies
             if use_dist:
                 dist.barrier()

@@ -73,6 +73,10 @@ def parser():
     ap.add_argument("--lpt", choices=["auto", "on", "off"], default="auto",
                     help="longest-expected-first dispatch of the children's local search (Island default: auto)")
     ap.add_argument("--lib", default=None, help="profiling: an A/B build (tools/ab_build.sh) instead of the in-tree library")
+    ap.add_argument("--schedule", choices=["batch", "staggered"], default="batch",
+                    help="Island schedule: whole generations, or two half-batches on two streams bred one "
+                         "half-batch behind (ttga.ga.Island)")
+    ap.add_argument("--parts", type=int, default=2, help="sub-batches of the staggered schedule")
     ap.add_argument("--islands", type=int, default=1,
                     help="K independent islands of --pop members on this GPU, each on its own stream (ttga.islands "
                          "--islands K between migrations); children/s over all K")
@@ -87,7 +91,8 @@ def run_ga(a):
     # island k's seed as ttga.islands gives it (ga.cpp:412); one island: --seed, no stream of its own
     seeds = [a.seed] + [rank_seed(a.seed, k) for k in range(1, K)]
     isls = [Island(dp, pop_size=a.pop, children=a.children, max_steps=a.steps, seed=seeds[k],
-                   lpt=None if a.lpt == "auto" else a.lpt == "on", stream=torch.cuda.Stream() if K > 1 else None)
+                   lpt=None if a.lpt == "auto" else a.lpt == "on", stream=torch.cuda.Stream() if K > 1 else None,
+                   schedule=a.schedule, parts=a.parts)
             for k in range(K)]
     isl = isls[0]
     torch.cuda.synchronize()
@@ -126,6 +131,8 @@ def run_ga(a):
         # the GPU idle while the host enqueued the next generation's launches)
         if gens >= a.gens and gens % 8 == 0:
             torch.cuda.synchronize()
+    for i in isls:
+        i.flush()                               # staggered: the last half-batch replaced inside the clock
     torch.cuda.synchronize()
     gpu_s = time.perf_counter() - t0
     feas, scv, hcv, pen = isl.member_meta(0)
@@ -137,7 +144,8 @@ def run_ga(a):
     pop_digest = _h.hexdigest()[:16]
     pf = isl.pop["feasible"].bool()
     out = {"config": a.config, "E": inst.E, "R": inst.R, "F": inst.F, "S": inst.S, "pop": a.pop,
-           "children_per_gen": a.children, "islands": K, "gens": gens, "max_steps": a.steps, "lpt_dispatch": isl.lpt,
+           "children_per_gen": a.children, "islands": K, "schedule": a.schedule,
+           "parts": isl.parts, "gens": gens, "max_steps": a.steps, "lpt_dispatch": isl.lpt,
            "init_seconds": init_s,
            "ls_phase2_step_share": ph2 / allsteps if allsteps else None,
            "warm_gens": warm, "feasible_fraction_at_start": feas_start,
