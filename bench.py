@@ -50,7 +50,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 POP_PER_GPU = 65536
 SIZE_NAMES = {"sm": "small01-size", "med": "medium01-size", "lg": "large01-size",
               "syn": "synthetic 2000/40/10/5000 scaling instance"}
-KERNELS = {2: "eval_block", 7: "eval_tile5", 8: "eval_tile5_w8", 9: "eval_tile6", 13: "eval_lanes_w16+eval_corr"}
+KERNELS = {2: "eval_block", 7: "eval_tile5", 8: "eval_tile5_w8", 13: "eval_lanes_w16+eval_corr"}
 
 
 def parse():
@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--global-pop", type=int, default=0,
                     help="individuals over all ranks, split across them (strong scaling); overrides --pop")
     ap.add_argument("--config", default="med", choices=["sm", "med", "lg", "syn"])
-    ap.add_argument("--variant", type=int, default=0, help="tt_eval kernel: 0 auto, 2 block, 7/8 tile5, 9 tile6, 13 wide path")
+    ap.add_argument("--variant", type=int, default=0, help="tt_eval kernel: 0 auto, 2 block, 7/8 tile5, 13 wide path")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="individuals in the CPU-baseline sample (0: sized to about --cpu-seconds of CPU work)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -139,7 +139,7 @@ def cpu_baseline(inst, slot_np, room_np, gpu_out):
             "cores_note": "every core this job may use (affinity and cgroup quota); the GPU box grants one GPU's share"}
 
 
-DOMINANT = {8: "eval_tile5_kernel", 9: "eval_tile6_kernel", 13: "eval_", 2: "eval_block_kernel"}   # kernel name substrings
+DOMINANT = {7: "eval_tile5_kernel", 8: "eval_tile5_kernel", 13: "eval_", 2: "eval_block_kernel"}   # kernel name substrings
 
 
 def visible_gpus() -> int:
@@ -264,9 +264,9 @@ def main():
         # off (tile5: lane and wave phase; wide path: eval_lanes only), which reads
         # exactly the P*E bytes of the slot rows with the kernel's own loads
         calib = list(child)
-        calib[-1] = str(v | (0x30 if v in (7, 8, 9) else 0x40 if v == 13 else 0))
+        calib[-1] = str(v | (0x30 if v in (7, 8) else 0x40 if v == 13 else 0))
         E = {"sm": 100, "syn": 2000}.get(args.config, 400)
-        pmc = pmc_live.derive(pmc_live.collect(child, DOMINANT.get(v, "eval_"), calib if v in (7, 8, 9, 13) else None),
+        pmc = pmc_live.derive(pmc_live.collect(child, DOMINANT.get(v, "eval_"), calib if v in (7, 8, 13) else None),
                               calib_bytes=float(P) * E)
     import torch
     import torch.distributed as dist

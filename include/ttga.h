@@ -80,9 +80,6 @@ int tt_eval(const tt_problem* p, const uint8_t* slot, const uint8_t* room, int P
  *   7/8 = eval_tile5, 4/8 waves per 64-individual tile (E <= 448): a
  *         lane-per-individual phase (attendance masks) and a wave-per-individual
  *         phase (bitset hard constraints), slot rows staged by LDS-DMA,
- *   9 = eval_tile6 (E <= 448): one 16-wave workgroup per CU takes the two
- *       phases of its tiles as a work queue (lane-phase chunks, then the 64
- *       individuals of each tile), two tile buffers, no barriers,
  *   13 = wide path: eval_lanes (16-wave lane-phase tile) + eval_corr (batches
  *        of individuals against the streamed correlation triangle; E <= 2490,
  *        the 64-row tile must fit the LDS; automatic for E > 448).
@@ -206,9 +203,6 @@ int tt_ga_replace(const tt_problem* p, uint8_t* pop_slot, uint8_t* pop_room, int
  *   bit 4 (16) the local search's per-stream redo list overflowed (unreachable:
  *              it holds P entries and a launch lists each wave at most once);
  *              the individuals not listed are left unsearched.
- *   bit 5 (32) eval_tile6 (tt_eval_variant 9) gave up waiting for a tile to be
- *              staged (unreachable: the work queue always drains, see
- *              csrc/tt_eval.hip; the bounded wait only guarantees termination).
  * Synchronises the device. */
 int tt_device_status(const tt_problem* p, int32_t* status);
 

@@ -196,7 +196,7 @@ __device__ __forceinline__ void corr_words(uint32_t bbase, const uint32_t* sv, c
 // the s_waitcnt itself. (Round 4 issued them from inline asm with a separate
 // wait; the compiler could copy the destination registers between issue and
 // wait -- a data race that showed up once as nondeterministic wide-path
-// results. tests/test_native.py::test_no_untracked_scalar_loads checks the
+// results. tests/test_codeobj.py::test_no_inline_asm_scalar_loads_in_sources checks the
 // built code object for asm-issued scalar loads.)
 template <int ST>
 __device__ __forceinline__ void sload_rec(const ConstU32* q, uint32_t (&r)[ST]) {
@@ -732,276 +732,6 @@ __global__ __launch_bounds__(64 * NW, 4) void eval_tile5_kernel(DevProblem pb, c
 #endif
 }
 
-// ---------------------------------------------------------------- eval_tile6
-// eval_tile5's two phases as a barrier-free work queue inside one 16-wave
-// workgroup per CU (variant 9). Round 4's workgroup stamps showed the cost of
-// one tile per workgroup: the wave arbiter favours a CU's older workgroup, so
-// of the two resident slots one finishes its tiles ~15 us early and the CU's
-// last workgroup runs alone (12 % idle slot time). Here a workgroup owns the
-// tiles blockIdx.x + k * gridDim.x and splits each into NI = NCH + 64 items:
-// NCH lane-phase chunks (student runs balanced by ids, srun_part) and the 64
-// wave-phase individuals. Waves take items from one LDS counter in order
-// (chunks of a tile before its individuals: the big items first), so no wave
-// idles while any item is left. Two tile buffers: the wave that completes a
-// tile's last item writes its outputs, stages tile k+2 into the freed buffer
-// (LDS-DMA) and publishes it; a wave that took an item of a tile not yet
-// staged waits on that buffer's ready word. A wave holds at most one started
-// item while it waits, and tile k+2 depends only on tile k's items, all taken
-// before any of k+2's, so the queue always drains; a bounded wait (status
-// bit 5, tested never to fire) guarantees termination regardless.
-constexpr int kT6Waves = 16;
-struct Tile6Layout {
-    int SP, WS;
-    size_t tile_bytes, off_ws, off_acc, off_ctl, bytes;
-};
-__host__ __device__ inline Tile6Layout tile6_layout(int E, int R) {
-    const Tile5Layout L5 = tile5_layout(E, R, kT6Waves, true);
-    Tile6Layout L;
-    L.SP = L5.SP; L.WS = L5.WS; L.tile_bytes = L5.tile_bytes;
-    L.off_ws = 2 * L.tile_bytes;
-    L.off_acc = L.off_ws + (size_t)kT6Waves * L.WS;              // part[2][64], hq[2][64]
-    L.off_ctl = L.off_acc + 4 * 4 * 64;                         // next, done[2], ready[2]
-    L.bytes = L.off_ctl + 64;
-    return L;
-}
-constexpr int kT6WaitBound = 1 << 22;           // s_sleep rounds before status bit 5 (never reached)
-
-// tile rows by byte copies (E % 4 != 0: no dword LDS-DMA), rows w0, w0 + nw, ...;
-// out of line, so the copy loop's registers stay out of the kernel's item loop
-__device__ __noinline__ void t6_stage_bytes(const uint8_t* src, uint8_t* dst, int n, int E, int SP, int w0, int nw) {
-    const int lane = threadIdx.x & 63;
-    for (int r = w0; r < n; r += nw)
-        for (int c = lane; c < E; c += 64) dst[r * SP + c] = src[(long)r * E + c];
-}
-
-template <int EWC, int PK, int NCH>
-__global__ __launch_bounds__(64 * kT6Waves, 1) void eval_tile6_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
-                                                                    const uint8_t* __restrict__ room, int P,
-                                                                    int32_t* __restrict__ hcv_out,
-                                                                    int32_t* __restrict__ scv_out,
-                                                                    uint8_t* __restrict__ feas_out,
-                                                                    int32_t* __restrict__ pen_out, int ablate_arg) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    constexpr int NW = kT6Waves, NI = NCH + 64;
-    const int ablate = ablate_arg & 3;
-    const int E = pb.E, R = pb.R;
-    const int lane = threadIdx.x & 63, wv = wave_id();
-    const Tile6Layout L = tile6_layout(E, R);
-    const int SP = L.SP;
-    uint8_t* ws = lds + L.off_ws + (size_t)wv * L.WS;
-    uint64_t* B = (uint64_t*)ws;                              // [45][EWC] event bitsets per slot
-    uint32_t* cnt = (uint32_t*)(B + kSlots * EWC);            // packed u16 cell counters
-    int32_t* part = (int32_t*)(lds + L.off_acc);              // [2][64] scv partials per buffer
-    int32_t* hq = part + 2 * 64;                              // [2][64] hcv (or -1)
-    int32_t* ctl = (int32_t*)(lds + L.off_ctl);               // [0] next item, [1..2] done, [3..4] ready
-    const int tiles = (P + 63) / 64;
-    const int my_tiles = (int)blockIdx.x < tiles ? (tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-    const int total = my_tiles * NI;
-    const bool last_partial = E < 64 * EWC;
-    const int RW = (R + 1) / 2;
-
-    using PossT = typename std::conditional<PK == 0, uint64_t, uint32_t>::type;
-    uint64_t inv_cup[EWC][EWC];
-    PossT inv_poss[EWC];
-    uint32_t inv_ps[EWC];
-    int inv_sn[EWC];
-#pragma unroll
-    for (int r = 0; r < EWC; ++r) {
-        const int e = lane + 64 * r;
-        const bool ok = e < E;
-        if constexpr (PK == 1) {
-            inv_ps[r] = ok ? ((~(uint32_t)pb.poss[e] & 0xFFFFu) | ((uint32_t)pb.sn[e] << 16)) : 0u;
-        } else {
-            inv_poss[r] = ok ? (PossT)pb.poss[e] : (PossT)~0ull;
-            inv_sn[r] = ok ? pb.sn[e] : 0;
-        }
-#pragma unroll
-        for (int w = 0; w < EWC; ++w) inv_cup[r][w] = (w >= r && ok) ? pb.cupT[(size_t)w * E + e] : 0ull;
-    }
-    const ConstI32* ptab = (const ConstI32*)pb.srun_part;
-    const int pbase = srun_part_base(NCH);
-    auto tile_of = [&](int k) { return (long)blockIdx.x + (long)k * gridDim.x; };
-    auto np_of = [&](int k) { return (int)min(64L, (long)P - tile_of(k) * 64); };
-
-    // set-up: counters, accumulators, sentinel columns, tiles 0 and 1 by every wave
-    if (threadIdx.x < 8) ctl[threadIdx.x] = threadIdx.x == 4 ? 1 : 0;       // ready[0] = 0, ready[1] = 1
-    if (threadIdx.x < 128) {
-        part[threadIdx.x] = 0;
-        lds[(threadIdx.x >> 6) * L.tile_bytes + (threadIdx.x & 63) * SP + E] = 63;
-    }
-    // LDS-DMA when the rows are dword-aligned, else byte copies (E % 4 != 0)
-    const bool dma = (E & 3) == 0 && (((uintptr_t)slot) & 3) == 0;
-    auto stage = [&](int k, uint8_t* dst, int w0, int nw) {
-        const uint8_t* src = slot + tile_of(k) * 64 * E;
-        const int n = np_of(k);
-        if (dma) {
-            if (nw == NW) tile_dma<NW>(src, dst, n, E, SP, w0, lane);
-            else tile_dma<1>(src, dst, n, E, SP, 0, lane);
-        } else {
-            t6_stage_bytes(src, dst, n, E, SP, w0, nw);
-        }
-    };
-    for (int k = 0; k < 2 && k < my_tiles; ++k) stage(k, lds + k * L.tile_bytes, wv, NW);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    auto grab = [&]() -> int {
-        int g = 0;
-        if (lane == 0) g = __hip_atomic_fetch_add(&ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return __builtin_amdgcn_readfirstlane(g);
-    };
-    // room row of individual q of tile k (buffer loads, 32-bit lane offsets)
-    auto load_row = [&](int k, int q, uint32_t* dst) {
-        const __amdgpu_buffer_rsrc_t rrs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(room + tile_of(k) * 64 * E), 0, 64 * E, 0x00020000);
-#pragma unroll
-        for (int r = 0; r < EWC; ++r)
-            dst[r] = (!last_partial || r < EWC - 1 || lane + 64 * r < E)
-                         ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rrs, lane + 64 * r, q * E, 0)
-                         : 0u;
-    };
-    auto individual = [&](int g, int& k, int& q) {              // item g -> tile k, individual q (or -1)
-        k = g / NI;
-        const int i = g - k * NI;
-        q = i >= NCH ? i - NCH : -1;
-    };
-
-    // LDS ordering: the DS instructions of one wave execute in issue order and the
-    // tile DMA has landed (vmcnt) before its ready word is written, so the queue
-    // words need no release/acquire fences -- only compiler barriers. (An acq_rel
-    // atomic waits for vmcnt(0), i.e. for the next individual's room-row prefetch,
-    // at every item.)
-    int seen[2] = {0, 1};                                      // ready words last seen per buffer
-    uint32_t pfn[EWC];
-    int cur = grab();
-    {
-        int k, q;
-        individual(cur, k, q);
-        if (cur < total && q >= 0 && q < np_of(k)) load_row(k, q, pfn);
-    }
-    while (cur < total) {
-        const int nxt = grab();
-        int k, q;
-        individual(cur, k, q);
-        const int b = k & 1;
-        uint32_t rv[EWC];
-#pragma unroll
-        for (int r = 0; r < EWC; ++r) rv[r] = pfn[r];
-        {
-            int k2, q2;
-            individual(nxt, k2, q2);
-            if (nxt < total && q2 >= 0 && q2 < np_of(k2)) load_row(k2, q2, pfn);     // next individual's rooms
-        }
-        // this item's tile must be staged
-        if ((b ? seen[1] : seen[0]) != k) {
-            int spins = 0;
-            while (__hip_atomic_load(&ctl[3 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != k) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins > kT6WaitBound) {
-                    if (lane == 0) atomicOr(pb.status, 32);
-                    break;
-                }
-            }
-            if (b) seen[1] = k; else seen[0] = k;
-            asm volatile("" ::: "memory");
-        }
-        const uint8_t* tile = lds + b * L.tile_bytes;
-        const int np = np_of(k);
-        if (q < 0) {
-            // ---- a lane-phase chunk (lane = individual): student runs of chunk i
-            const int i = cur - k * NI;
-            const int r0 = ptab[pbase + i], r1 = ptab[pbase + i + 1];
-            if (!(ablate & 1) && r0 < r1) {
-                uint32_t lsp;
-                asm volatile("v_mul_u32_u24 %0, %1, %2" : "=v"(lsp) : "v"(lane), "s"(SP));
-                const int sc = lane_scv_runs<1>(tile + lsp, pb, r0, r1);
-                __hip_atomic_fetch_add(&part[b * 64 + lane], sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        } else if (q < np) {
-            // ---- a wave-phase individual (wave = individual): hcv terms + last-slot term
-            uint32_t sv[EWC];
-            const uint8_t* rs = tile + q * SP;
-#pragma unroll
-            for (int r = 0; r < EWC; ++r)
-                sv[r] = (!last_partial || r < EWC - 1 || lane + 64 * r < E) ? rs[lane + 64 * r] : 0u;
-            uint32_t smax = 0, rmax = 0;
-#pragma unroll
-            for (int r = 0; r < EWC; ++r) { smax = max(smax, sv[r]); rmax = max(rmax, rv[r]); }
-            const bool any_bad = wave_any(smax >= (uint32_t)kSlots || rmax >= (uint32_t)R);
-            int h = 0, last = 0;
-            if (!any_bad && !(ablate & 2)) {
-                for (int c = lane; c < (L.WS >> 4); c += 64) ((uint4*)ws)[c] = make_uint4(0u, 0u, 0u, 0u);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-                for (int r = 0; r < EWC; ++r) {
-                    if (r < EWC - 1 || !last_partial || lane + 64 * r < E) {
-                        const uint32_t s = sv[r], ro = rv[r];
-                        atomicOr((unsigned long long*)&B[s * EWC + r], 1ull << lane);
-                        uint32_t* c = (uint32_t*)((uint8_t*)cnt + ((__umul24(s, (uint32_t)(2 * RW)) + (ro & ~1u)) << 1));
-                        const uint32_t sh = ro << 4;
-                        h += (int)__builtin_amdgcn_ubfe(atomicAdd(c, 1u << (sh & 31u)), sh, 16);   // :148-150
-                        if constexpr (PK == 1) {
-                            h += (int)__builtin_amdgcn_ubfe(inv_ps[r], ro, 1);                         // :155-156
-                            last = (int)mad_u16_hi((uint32_t)(kLastSlotMask >> s) & 1u, inv_ps[r], (uint32_t)last);
-                        } else {
-                            h += (int)(((inv_poss[r] >> ro) & 1u) ^ 1u);
-                            last += ((kLastSlotMask >> s) & 1ull) ? inv_sn[r] : 0;                       // :93-96
-                        }
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                corr_words<0, EWC>(lds_addr(B), sv, inv_cup, lane, E, last_partial, h);               // :151-153
-                if (!wave_any(h >= 1024 || last >= 1024)) {
-                    const uint32_t t = (uint32_t)wave_sum((h << 16) | last);
-                    h = (int)(t >> 16);
-                    last = (int)(t & 0xFFFFu);
-                } else {
-                    h = wave_sum(h);
-                    last = wave_sum(last);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
-            if (lane == 0) {
-                hq[b * 64 + q] = any_bad ? -1 : h;
-                if (last) __hip_atomic_fetch_add(&part[b * 64 + q], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        }
-        // ---- item done; the wave that completes the tile writes it out and stages tile k + 2
-        int old = 0;
-        asm volatile("" ::: "memory");
-        if (lane == 0) old = __hip_atomic_fetch_add(&ctl[1 + b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        old = __builtin_amdgcn_readfirstlane(old);
-        asm volatile("" ::: "memory");
-        if (old == NI - 1) {
-            const int kn = k + 2;
-            if (kn < my_tiles) stage(kn, lds + b * L.tile_bytes, 0, 1);
-            if (lane < np) {
-                const long p = tile_of(k) * 64 + lane;
-                const int h = hq[b * 64 + lane], s2 = part[b * 64 + lane];
-                if (h < 0) {
-                    hcv_out[p] = -1; scv_out[p] = -1; feas_out[p] = 0; pen_out[p] = -1;
-                } else {
-                    hcv_out[p] = h;
-                    scv_out[p] = s2;
-                    feas_out[p] = h == 0 ? 1 : 0;
-                    pen_out[p] = h == 0 ? s2 : 1000000 + h;
-                }
-            }
-            part[b * 64 + lane] = 0;
-            if (lane == 0) ctl[1 + b] = 0;
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // the DMA has landed, the resets are done
-            if (lane == 0) __hip_atomic_store(&ctl[3 + b], kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        cur = nxt;
-    }
-}
-
 // ---------------------------------------------------------------- eval_lanes
 // The lane phase of eval_tile5 on its own (wide path, E > 448): a 16-wave
 // workgroup per 64-row tile (128 KB at E = 2000: one workgroup per CU); it
@@ -1486,10 +1216,6 @@ static bool tile5_fits(const tt_problem* p, int NW) {
     return p->dev.EW64 <= 7 && p->E <= 32767 && tile5_layout(p->E, p->R, NW).bytes <= (NW == 8 ? 80 : 160) * 1024;
 }
 
-static bool tile6_fits(const tt_problem* p) {
-    return p->dev.EW64 <= 7 && p->E <= 448 && tile6_layout(p->E, p->R).bytes <= 160 * 1024;
-}
-
 static bool wide_fits(const tt_problem* p) {
     const int EW64 = p->dev.EW64;
     return p->E <= 32767 && lanes_lds_bytes(p->E) <= 160 * 1024 &&
@@ -1532,8 +1258,8 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
     // eval_corr build phase, 2 eval_corr corr phase, 4 no eval_corr launch
     const int ablate = variant >> 4;
     variant &= 15;
-    if (variant != 0 && variant != 2 && variant != 7 && variant != 8 && variant != 9 && variant != 13) {
-        set_error("unknown eval variant (0 auto, 2 block, 7/8 tile5, 9 tile6, 13 wide)");
+    if (variant != 0 && variant != 2 && variant != 7 && variant != 8 && variant != 13) {
+        set_error("unknown eval variant (0 auto, 2 block, 7/8 tile5, 13 wide)");
         return TT_ERR_INVALID;
     }
     if (P == 0) return TT_OK;
@@ -1552,6 +1278,7 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
             auto launch_l = [&](auto kern) -> int {
                 int per_cu = 0;
                 TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 1024, lds_l));
+                per_cu = std::min(per_cu, lds_resident_limit(lds_l));    // the 1,280-B LDS block rule
                 const int grid = std::min(tiles, std::max(1, per_cu) * p->num_cus);
                 hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), lds_l, st, p->dev, slot, P, scv);
                 return TT_OK;
@@ -1565,6 +1292,7 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
         auto launch = [&](auto kern) -> int {
             int per_cu = 0;
             TT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * CL.NWV, CL.bytes));
+            per_cu = std::min(per_cu, lds_resident_limit(CL.bytes));
             const long batches = ((long)P + NB - 1) / NB;
             const int grid = (int)std::min<long>(batches, (long)std::max(1, per_cu) * p->num_cus);
             hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * CL.NWV), CL.bytes, st, p->dev, slot, room, P, hcv, scv,
@@ -1647,29 +1375,6 @@ extern "C" int tt_eval_variant(const tt_problem* p, const uint8_t* slot, const u
 #undef TT_T5
 #undef TT_T5N
 #undef TT_T5U
-        if (rc) return rc;
-    } else if (variant == 9) {
-        // eval_tile6: one 16-wave workgroup per CU, tiles as a work queue of items
-        if (!tile6_fits(p)) {
-            set_error("instance outside the tile6 kernel (E <= 448)");
-            return TT_ERR_LIMIT;
-        }
-        const Tile6Layout L6 = tile6_layout(E, R);
-        const int pk = (R <= 16 && p->max_sn <= 0xFFFF) ? 1 : R <= 32 ? 2 : 0;
-        const int grid = std::min((P + 63) / 64, p->num_cus);
-#define TT_T6U(EWC, PKV) \
-    hipLaunchKernelGGL((eval_tile6_kernel<EWC, PKV, 16>), dim3(grid), dim3(64 * kT6Waves), L6.bytes, st, p->dev, slot, \
-                       room, P, hcv, scv, feasible, penalty, ablate);
-#define TT_T6(EWC)                                                                     \
-    case EWC:                                                                          \
-        if (pk == 1) { TT_T6U(EWC, 1) } else if (pk == 2) { TT_T6U(EWC, 2) } else { TT_T6U(EWC, 0) } \
-        break;
-        switch (p->dev.EW64) {
-            TT_T6(1) TT_T6(2) TT_T6(3) TT_T6(4) TT_T6(5) TT_T6(6) TT_T6(7)
-            default: rc = TT_ERR_LIMIT; break;
-        }
-#undef TT_T6
-#undef TT_T6U
         if (rc) return rc;
     } else {
         const size_t lds = block_lds_bytes(E, R);

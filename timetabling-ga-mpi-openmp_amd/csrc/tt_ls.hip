@@ -637,6 +637,14 @@ struct TaskRegs {
     uint64_t tpl[3];
 };
 
+// TT_LS_TASK_LATE: a task's events and possible rooms are loaded in the task
+// loop right before its matching, instead of all three tasks' at once ahead of
+// the loop: the 12 VGPRs of the early form stay live across the inlined
+// matcher, which at the kernel's 96 VGPRs spilled them to scratch (the largest
+// group of the kernel's scratch accesses)
+#ifndef TT_LS_TASK_LATE
+#define TT_LS_TASK_LATE 1
+#endif
 // every task's events and possible rooms into registers at once (one L2 round
 // trip), issued as early as the trial allows so the latency overlaps other work
 __device__ __forceinline__ TaskRegs load_tasks(LsState& S, int kmask) {
@@ -647,6 +655,11 @@ __device__ __forceinline__ TaskRegs load_tasks(LsState& S, int kmask) {
         S.listed = 1;
     }
     TaskRegs r;
+    if (TT_LS_TASK_LATE) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { r.tn[k] = 0; r.tev[k] = 0; r.tpl[k] = 0ull; }
+        return r;
+    }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         r.tn[k] = k < S.nts && ((kmask >> k) & 1) ? S.misc[4 + k] : 0;
@@ -671,9 +684,18 @@ __device__ __forceinline__ bool match_tasks(LsState& S, int kmask, const TaskReg
     for (int k = 0; k < 3; ++k) {
         if (k >= S.nts) break;
         if (!((kmask >> k) & 1)) continue;
-        const int N = k == 0 ? tr.tn[0] : k == 1 ? tr.tn[1] : tr.tn[2];
-        const int tevk = k == 0 ? tr.tev[0] : k == 1 ? tr.tev[1] : tr.tev[2];
-        const uint64_t tplk = k == 0 ? tr.tpl[0] : k == 1 ? tr.tpl[1] : tr.tpl[2];
+        int N, tevk;
+        uint64_t tplk;
+        if (TT_LS_TASK_LATE) {
+            N = __builtin_amdgcn_readfirstlane(S.misc[4 + k]);
+            const bool a = S.lane < N && N <= 64;
+            tevk = a ? get_task(S, k).ev[S.lane] : 0;
+            tplk = a ? poss_of(S, tevk) : 0ull;
+        } else {
+            N = k == 0 ? tr.tn[0] : k == 1 ? tr.tn[1] : tr.tn[2];
+            tevk = k == 0 ? tr.tev[0] : k == 1 ? tr.tev[1] : tr.tev[2];
+            tplk = k == 0 ? tr.tpl[0] : k == 1 ? tr.tpl[1] : tr.tpl[2];
+        }
         if (N > S.NT) {                                             // task capacity exceeded
             if (S.lane == 0) {
                 if (S.NT < kMaxSlotEvents && S.NT < S.E) {
@@ -1035,8 +1057,28 @@ __device__ __forceinline__ SinfView sinf_view(const LsState& S) {
     return SinfView{S.sinf, S.B, S.sl, S.rr, S.ps, S.pb.poss, S.task_base, S.E, S.R, S.EW, S.scratch};
 }
 __device__ __forceinline__ uint64_t vposs(const SinfView& V, int e) { return V.ps ? (uint64_t)V.ps[e] : V.poss[e]; }
+// TT_LS_SINF_REGS: the out-of-line functions take the view's fields as plain
+// arguments (registers) instead of the aggregate by value, which sits in the
+// caller's scratch frame (72 B). Same-box A/B (profiles/r06_ab_ls_scratch.jsonl):
+// 48 B less scratch, but the 19 argument VGPRs at the call sites cost LS(200)
+// +5..10 %; off.
+#ifndef TT_LS_SINF_REGS
+#define TT_LS_SINF_REGS 0
+#endif
+#if TT_LS_SINF_REGS
+#define TT_SINF_PARAMS                                                                                          \
+    SlotInfo *v_sinf, const uint64_t *v_B, const uint8_t *v_sl, const uint8_t *v_rr, const uint16_t *v_ps,      \
+        const uint64_t *v_poss, uint8_t *v_task_base, int v_E, int v_R, int v_EW, int v_scratch
+#define TT_SINF_VIEW SinfView{v_sinf, v_B, v_sl, v_rr, v_ps, v_poss, v_task_base, v_E, v_R, v_EW, v_scratch}
+#define TT_SINF_ARGS(V) (V).sinf, (V).B, (V).sl, (V).rr, (V).ps, (V).poss, (V).task_base, (V).E, (V).R, (V).EW, (V).scratch
+#else
+#define TT_SINF_PARAMS SinfView v_view
+#define TT_SINF_VIEW v_view
+#define TT_SINF_ARGS(V) (V)
+#endif
 
-__device__ __noinline__ void sinf_build_v(SinfView V, int t) {
+__device__ __noinline__ void sinf_build_v(TT_SINF_PARAMS, int t) {
+    const SinfView V = TT_SINF_VIEW;
     const int R = V.R, EW = V.EW, lane = threadIdx.x & 63;
     uint16_t* own = (uint16_t*)V.task_base;               // scratch: free after accept's hist copies
     if (lane < R) own[lane] = 0xFFFF;
@@ -1079,7 +1121,10 @@ __device__ __noinline__ void sinf_build_v(SinfView V, int t) {
     }
     wave_sync();
 }
-__device__ __forceinline__ void sinf_build(LsState& S, int t) { sinf_build_v(sinf_view(S), t); }
+__device__ __forceinline__ void sinf_build(LsState& S, int t) {
+    const SinfView V = sinf_view(S);
+    sinf_build_v(TT_SINF_ARGS(V), t);
+}
 
 // lower bound on the clash pairs of slot s minus `out` (-1: none) plus event a
 // after the reference's re-match (0 for an untrusted slot); any lanes
@@ -1100,11 +1145,12 @@ __device__ __forceinline__ int pairs_lb(LsState& S, int s, int out, int a) {
 // (free at this point), then the used masks, the fr fixed point over all
 // slots together, and the maximality check (sinf_build slot by slot when
 // the 45 x R owner table does not fit the task scratch)
-__device__ __noinline__ void sinf_init_v(SinfView V) {
+__device__ __noinline__ void sinf_init_v(TT_SINF_PARAMS) {
+    const SinfView V = TT_SINF_VIEW;
     const int E = V.E, R = V.R, lane = threadIdx.x & 63;
     const int NC = kSlots * R;
     if ((size_t)2 * NC > (size_t)V.scratch) {
-        for (int t = 0; t < kSlots; ++t) sinf_build_v(V, t);
+        for (int t = 0; t < kSlots; ++t) sinf_build_v(TT_SINF_ARGS(V), t);
         return;
     }
     uint16_t* own2 = (uint16_t*)V.task_base;                    // [45][R]
@@ -1151,7 +1197,8 @@ __device__ __noinline__ void sinf_init_v(SinfView V) {
 }
 __device__ __forceinline__ void sinf_init(LsState& S) {
     LSP_T(t0);
-    sinf_init_v(sinf_view(S));
+    const SinfView V = sinf_view(S);
+    sinf_init_v(TT_SINF_ARGS(V));
     LSP_ADD(S, kPfBInit, t0);
 }
 
