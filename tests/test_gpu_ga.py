@@ -373,6 +373,30 @@ def test_ga_trajectories_match_reference_statistically(sm):
     _assert_same_quality(stats, seeds, dfinal, dfeas, rtrace[:, -1], rfeas)
 
 
+def test_ga_staggered_trajectories_match_reference_statistically(sm):
+    """The staggered schedule against the reference's ga.cpp loop (fresh
+    crossover child), same number of children: the device GA with two
+    sub-batches of one child (pop 10, C = 2, each child bred one child behind,
+    as two ga.cpp threads would) for 500 generations against the reference's
+    one-thread loop for 1000 generations, 16 seeds, maxSteps 200 on sm. Same
+    feasibility (Fisher), no shift of the final best (Mann-Whitney U, p >
+    0.01), medians within 20 %."""
+    from oracle_lib import ref
+    R = ref()
+    if R is None:
+        pytest.skip("reference build oracle/_ref not present")
+    stats = pytest.importorskip("scipy.stats")
+    sys.path.insert(0, str(REPO / "tools"))
+    from ga_quality import device_runs
+    from oracle_lib import host_threads
+    inst = sm[0]
+    seeds = list(range(1, 17))
+    _, _, rfeas, _, rtrace, _ = R.problem(inst).ga_run(seeds, 10, 1000, 200, 0, host_threads())
+    dfinal, dfeas, dtrace, _ = device_runs(inst, seeds, 10, 500, 200, children=2, schedule="staggered")
+    assert np.all(np.diff(dtrace, axis=1) <= 0)
+    _assert_same_quality(stats, seeds, dfinal, dfeas, rtrace[:, -1], rfeas)
+
+
 def _assert_same_quality(stats, seeds, dfinal, dfeas, rfinal, rfeas):
     """Same feasibility count (Fisher), no shift of the final best (Mann-Whitney
     U, p > 0.01), device median best within 20 % of the reference's."""

@@ -47,7 +47,7 @@ def summarize(final, feas, trace, checkpoints):
     }
 
 
-def device_runs(inst, seeds, pop, gens, steps):
+def device_runs(inst, seeds, pop, gens, steps, children=1, schedule="batch"):
     import torch
 
     from ttga import native
@@ -58,7 +58,7 @@ def device_runs(inst, seeds, pop, gens, steps):
     trace = np.zeros((len(seeds), gens + 1), np.int64)
     secs = []
     for k, s in enumerate(seeds):
-        isl = Island(dp, pop_size=pop, children=1, max_steps=steps, seed=int(s))
+        isl = Island(dp, pop_size=pop, children=children, max_steps=steps, seed=int(s), schedule=schedule)
         tr = torch.zeros(gens + 1, dtype=torch.int64, device="cuda")
         p = isl.pop
 
@@ -73,6 +73,8 @@ def device_runs(inst, seeds, pop, gens, steps):
         for g in range(gens):
             isl.step()
             log(g + 1)
+        isl.flush()                      # staggered: the pending sub-batches replaced
+        log(gens)
         torch.cuda.synchronize()
         secs.append(time.perf_counter() - t0)
         trace[k] = tr.cpu().numpy()
@@ -91,9 +93,22 @@ def main():
     ap.add_argument("--pop", type=int, default=10)
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--no-device", action="store_true")
+    ap.add_argument("--device-children", type=int, default=1, help="children per device generation")
+    ap.add_argument("--device-gens", type=int, default=0, help="device generations (0: --gens)")
+    ap.add_argument("--device-schedule", choices=["batch", "staggered"], default="batch")
+    ap.add_argument("--no-ref-as-is", action="store_true", help="skip the reference run with F2")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     from scipy import stats
+
+    import threading
+    t_start = time.perf_counter()
+
+    def heartbeat():                     # the long reference runs print nothing for minutes
+        while True:
+            time.sleep(30)
+            print(f"[ga_quality] running {time.perf_counter() - t_start:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
 
     from oracle_lib import ref
     inst = ttga.config_instance(a.config)
@@ -107,7 +122,7 @@ def main():
     if R is None:
         raise SystemExit("oracle/_ref/libttref.so is missing (build it where /root/reference exists)")
     h = R.problem(inst)
-    for name, as_is in (("reference_as_is", 1), ("reference_fresh_child", 0)):
+    for name, as_is in ((("reference_as_is", 1),) if not a.no_ref_as_is else ()) + (("reference_fresh_child", 0),):
         hcv, scv, feas, pen, trace, secs = h.ga_run(seeds, a.pop, a.gens, a.steps, as_is, threads)
         final = trace[:, -1]
         res["runs"][name] = summarize(final, feas, trace, checkpoints)
@@ -115,12 +130,15 @@ def main():
         res["runs"][name]["note"] = ("ref_ga_run, OpenMP over seeds (%d threads); seconds_per_run = wall x "
                                      "threads / runs" % threads)
     if not a.no_device:
-        final, feas, trace, secs = device_runs(inst, seeds, a.pop, a.gens, a.steps)
-        res["runs"]["device"] = summarize(final, feas, trace, checkpoints)
+        dg = a.device_gens or a.gens
+        final, feas, trace, secs = device_runs(inst, seeds, a.pop, dg, a.steps, a.device_children, a.device_schedule)
+        res["runs"]["device"] = summarize(final, feas, trace, sorted({0, dg // 2, dg}))
         res["runs"]["device"]["seconds_per_run"] = secs
-        res["runs"]["device"]["note"] = "ttga.ga.Island(pop_size, children=1), one island at a time on cuda:0"
+        res["runs"]["device"]["note"] = (f"ttga.ga.Island(pop_size, children={a.device_children}, schedule="
+                                         f"{a.device_schedule}), {dg} generations ({dg * a.device_children} children; "
+                                         f"the reference: {a.gens}), one island at a time on cuda:0")
         tests = {}
-        for name in ("reference_as_is", "reference_fresh_child"):
+        for name in [n for n in ("reference_as_is", "reference_fresh_child") if n in res["runs"]]:
             r = res["runs"][name]
             fa = np.array([v < 1000000 for v in r["final_log_value"]])
             fd = feas.astype(bool)

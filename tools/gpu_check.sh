@@ -60,6 +60,9 @@ for s in $STEPS; do
     stagtests) run pytest_stag 900 python -u -m pytest tests/test_gpu_ga.py -m gpu -v --timeout 300 --timeout-method thread -k "staggered or island_generations or breed_vs or replace_vs" ;;
     gastag) for c in ${STAGCFGS:-comp15 comp16 comp10 comp01}; do for sch in ${STAGSCH:-batch staggered}; do for np in ${STAGPARTS:-2}; do run ga8k_${c}_${sch}_$np 400 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample ${CPUS:-0} --schedule $sch --parts $np; done; done; done ;;
     lsroof) run ls_roofline 1100 python -u tools/ls_roofline.py ${LSROOF:---config comp01 --config comp10 --config comp15} --out "$OUT/ls_roofline.jsonl" ;;
+    gacomps20s) run ga_comps20_stag 1100 python -u tools/ga_comps.py "$OUT/ga_comps20_staggered.json" --schedule staggered ;;
+    qualstag) run ga_quality_sm_stag 600 python -u tools/ga_quality.py --config sm --seeds 16 --gens 2001 --steps 200 --device-children 2 --device-gens 1000 --device-schedule staggered --out "$OUT/ga_quality_sm_staggered.json" &&
+              run ga_quality_med_stag 900 python -u tools/ga_quality.py --config med --seeds 16 --gens 2001 --steps 1000 --device-children 2 --device-gens 1000 --device-schedule staggered --no-ref-as-is --out "$OUT/ga_quality_med_staggered.json" ;;
     gatests) run pytest_ga 600 python -u -m pytest tests/test_gpu_ga.py -m gpu -v --timeout 300 --timeout-method thread ;;
     derive) run pytest_derive 400 python -u -m pytest tests/test_gpu_derive.py -m gpu -v --timeout 200 --timeout-method thread ;;
     newtests) run pytest_new 600 python -u -m pytest tests/test_gpu_derive.py tests/test_gpu_ga.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread -k "derive or derived or permutation or redo" ;;
