@@ -136,6 +136,23 @@ class Members:
         return (True, b[1]) if b[0] else (False, b[2] * 1000000 + b[1])
 
 
+_SIDE_STREAMS: dict = {}
+
+
+def _side_streams(dev, base, n: int) -> list:
+    """n streams for a staggered island's parts 1..n, cached per (device, base
+    stream): islands built one after another on the same base stream reuse the
+    same side streams. (A process gets a few hardware queues, GPU_MAX_HW_QUEUES,
+    and HIP maps streams onto them as they are created: fresh streams per
+    island can land on the queue of the base stream and serialise the parts.)"""
+    import torch
+    key = (dev.index, None if base is None else base.cuda_stream)
+    pool = _SIDE_STREAMS.setdefault(key, [])
+    while len(pool) < n:
+        pool.append(torch.cuda.Stream(dev))
+    return pool[:n]
+
+
 class Island(Members):
     """One island: population [N] + C child slots, all device-resident.
 
@@ -202,7 +219,7 @@ class Island(Members):
             for d in self._part:
                 r = d["rows"]
                 d.update(child={k: v[r] for k, v in self.child.items()}, rng=self.rng_child[r], flags=self.flags[r])
-            self._streams = [stream] + [torch.cuda.Stream(dev) for _ in range(self.parts - 1)]
+            self._streams = [stream] + _side_streams(dev, stream, self.parts - 1)
             self._ev_op = torch.cuda.Event()          # the last population operation (breed or replace)
             self._pending = []                        # parts searched but not yet replaced, in breed order
             self._last_replace = 0                    # part whose work buffer holds the last replace's source
