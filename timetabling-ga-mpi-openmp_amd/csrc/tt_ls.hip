@@ -1057,25 +1057,54 @@ __device__ __forceinline__ SinfView sinf_view(const LsState& S) {
     return SinfView{S.sinf, S.B, S.sl, S.rr, S.ps, S.pb.poss, S.task_base, S.E, S.R, S.EW, S.scratch};
 }
 __device__ __forceinline__ uint64_t vposs(const SinfView& V, int e) { return V.ps ? (uint64_t)V.ps[e] : V.poss[e]; }
-// TT_LS_SINF_REGS: the out-of-line functions take the view's fields as plain
-// arguments (registers) instead of the aggregate by value, which sits in the
-// caller's scratch frame (72 B). Same-box A/B (profiles/r06_ab_ls_scratch.jsonl):
-// 48 B less scratch, but the 19 argument VGPRs at the call sites cost LS(200)
-// +5..10 %; off.
-#ifndef TT_LS_SINF_REGS
-#define TT_LS_SINF_REGS 0
-#endif
-#if TT_LS_SINF_REGS
-#define TT_SINF_PARAMS                                                                                          \
-    SlotInfo *v_sinf, const uint64_t *v_B, const uint8_t *v_sl, const uint8_t *v_rr, const uint16_t *v_ps,      \
-        const uint64_t *v_poss, uint8_t *v_task_base, int v_E, int v_R, int v_EW, int v_scratch
-#define TT_SINF_VIEW SinfView{v_sinf, v_B, v_sl, v_rr, v_ps, v_poss, v_task_base, v_E, v_R, v_EW, v_scratch}
-#define TT_SINF_ARGS(V) (V).sinf, (V).B, (V).sl, (V).rr, (V).ps, (V).poss, (V).task_base, (V).E, (V).R, (V).EW, (V).scratch
-#else
-#define TT_SINF_PARAMS SinfView v_view
-#define TT_SINF_VIEW v_view
+// The out-of-line summary functions get their view through LDS: sinf_init writes
+// it into the wave's misc words [kSinfViewMisc, +12) -- LDS byte offsets of the
+// arrays, the global possibleRooms pointer as two words, E, R, EW and the task
+// scratch size -- and the functions take one pointer to it. (A SinfView passed
+// by value is an aggregate in the caller's scratch frame, 72 B per lane; its
+// fields as 19 argument registers measured +5..10 % on LS(200) from the call
+// sites' register pressure, profiles/r06_ab_ls_scratch.jsonl.)
+constexpr int kSinfViewMisc = 12;
+extern __shared__ __attribute__((aligned(16))) uint8_t tt_ls_dyn[];   // the kernel's dynamic LDS
+__device__ __forceinline__ void sinf_store_view(const LsState& S) {
+    const int lane = S.lane;
+    if (lane < 12) {
+        const auto off = [](const void* q) { return q ? (int32_t)((const uint8_t*)q - tt_ls_dyn) : -1; };
+        const uint64_t gp = (uint64_t)(uintptr_t)S.pb.poss;
+        int32_t v = 0;
+        switch (lane) {
+            case 0: v = off(S.sinf); break;
+            case 1: v = off(S.B); break;
+            case 2: v = off(S.sl); break;
+            case 3: v = off(S.rr); break;
+            case 4: v = off(S.ps); break;
+            case 5: v = off(S.task_base); break;
+            case 6: v = (int32_t)(uint32_t)gp; break;
+            case 7: v = (int32_t)(uint32_t)(gp >> 32); break;
+            case 8: v = S.E; break;
+            case 9: v = S.R; break;
+            case 10: v = S.EW; break;
+            default: v = S.scratch; break;
+        }
+        S.misc[kSinfViewMisc + lane] = v;
+    }
+    wave_sync();
+}
+__device__ __forceinline__ SinfView sinf_load_view(const int32_t* mv) {
+    SinfView V;
+    V.sinf = (SlotInfo*)(tt_ls_dyn + mv[0]);
+    V.B = (const uint64_t*)(tt_ls_dyn + mv[1]);
+    V.sl = tt_ls_dyn + mv[2];
+    V.rr = tt_ls_dyn + mv[3];
+    V.ps = mv[4] < 0 ? nullptr : (const uint16_t*)(tt_ls_dyn + mv[4]);
+    V.task_base = tt_ls_dyn + mv[5];
+    V.poss = (const uint64_t*)(uintptr_t)(((uint64_t)(uint32_t)mv[7] << 32) | (uint32_t)mv[6]);
+    V.E = mv[8]; V.R = mv[9]; V.EW = mv[10]; V.scratch = mv[11];
+    return V;
+}
+#define TT_SINF_PARAMS const int32_t *v_mv
+#define TT_SINF_VIEW sinf_load_view(v_mv)
 #define TT_SINF_ARGS(V) (V)
-#endif
 
 __device__ __noinline__ void sinf_build_v(TT_SINF_PARAMS, int t) {
     const SinfView V = TT_SINF_VIEW;
@@ -1122,8 +1151,7 @@ __device__ __noinline__ void sinf_build_v(TT_SINF_PARAMS, int t) {
     wave_sync();
 }
 __device__ __forceinline__ void sinf_build(LsState& S, int t) {
-    const SinfView V = sinf_view(S);
-    sinf_build_v(TT_SINF_ARGS(V), t);
+    sinf_build_v(S.misc + kSinfViewMisc, t);                  // the view sinf_init stored
 }
 
 // lower bound on the clash pairs of slot s minus `out` (-1: none) plus event a
@@ -1150,7 +1178,7 @@ __device__ __noinline__ void sinf_init_v(TT_SINF_PARAMS) {
     const int E = V.E, R = V.R, lane = threadIdx.x & 63;
     const int NC = kSlots * R;
     if ((size_t)2 * NC > (size_t)V.scratch) {
-        for (int t = 0; t < kSlots; ++t) sinf_build_v(TT_SINF_ARGS(V), t);
+        for (int t = 0; t < kSlots; ++t) sinf_build_v(v_mv, t);
         return;
     }
     uint16_t* own2 = (uint16_t*)V.task_base;                    // [45][R]
@@ -1197,8 +1225,8 @@ __device__ __noinline__ void sinf_init_v(TT_SINF_PARAMS) {
 }
 __device__ __forceinline__ void sinf_init(LsState& S) {
     LSP_T(t0);
-    const SinfView V = sinf_view(S);
-    sinf_init_v(TT_SINF_ARGS(V));
+    sinf_store_view(S);
+    sinf_init_v(S.misc + kSinfViewMisc);
     LSP_ADD(S, kPfBInit, t0);
 }
 
