@@ -63,6 +63,8 @@ for s in $STEPS; do
     gacomps20s) run ga_comps20_stag 1100 python -u tools/ga_comps.py "$OUT/ga_comps20_staggered.json" --schedule staggered ;;
     qualstag) run ga_quality_sm_stag 600 python -u tools/ga_quality.py --config sm --seeds 16 --gens 2001 --steps 200 --device-children 2 --device-gens 1000 --device-schedule staggered --out "$OUT/ga_quality_sm_staggered.json" &&
               run ga_quality_med_stag 900 python -u tools/ga_quality.py --config med --seeds 16 --gens 2001 --steps 1000 --device-children 2 --device-gens 1000 --device-schedule staggered --no-ref-as-is --out "$OUT/ga_quality_med_staggered.json" ;;
+    t5parts) run t5_components 600 python -u tools/t5_components.py ab_libs/libttga_abl.so med 65536 ;;
+    abt5x) for c in ${T5CFGS:-med lg comp01 med}; do run ab_t5_$c 300 python -u tools/ab_eval.py $c 65536 $T5SPECS; done ;;
     gatests) run pytest_ga 600 python -u -m pytest tests/test_gpu_ga.py -m gpu -v --timeout 300 --timeout-method thread ;;
     derive) run pytest_derive 400 python -u -m pytest tests/test_gpu_derive.py -m gpu -v --timeout 200 --timeout-method thread ;;
     newtests) run pytest_new 600 python -u -m pytest tests/test_gpu_derive.py tests/test_gpu_ga.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread -k "derive or derived or permutation or redo" ;;
