@@ -65,6 +65,10 @@ for s in $STEPS; do
               run ga_quality_med_stag 900 python -u tools/ga_quality.py --config med --seeds 16 --gens 2001 --steps 1000 --device-children 2 --device-gens 1000 --device-schedule staggered --no-ref-as-is --out "$OUT/ga_quality_med_staggered.json" ;;
     t5parts) run t5_components 600 python -u tools/t5_components.py ab_libs/libttga_abl.so med 65536 ;;
     abt5x) for c in ${T5CFGS:-med lg comp01 med}; do run ab_t5_$c 300 python -u tools/ab_eval.py $c 65536 $T5SPECS; done ;;
+    stagtrace) for sch in batch staggered; do n=20; [ $sch = staggered ] && n=40
+                 run trace_$sch 400 rocprofv3 --kernel-trace -d "$OUT/tr_$sch" -o run --output-format csv -- python -u tools/bench_ga.py --config ${TRCFG:-comp20} --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 20 --cpu-sample 0 --schedule $sch &&
+                 python tools/trace_window.py "$OUT/tr_$sch/run_kernel_trace.csv" $n > "$OUT/trace_window_$sch.json" && python tools/trace_overlap.py "$OUT/tr_$sch/run_kernel_trace.csv" --last $n > "$OUT/trace_overlap_$sch.json"; done ;;
+    stagl) for c in ${STAGCFGS:-comp20 comp15}; do for l in on off; do run ga8k_${c}_stag_lpt$l 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --schedule staggered --lpt $l; done; run ga8k_${c}_batch 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0; done ;;
     gatests) run pytest_ga 600 python -u -m pytest tests/test_gpu_ga.py -m gpu -v --timeout 300 --timeout-method thread ;;
     derive) run pytest_derive 400 python -u -m pytest tests/test_gpu_derive.py -m gpu -v --timeout 200 --timeout-method thread ;;
     newtests) run pytest_new 600 python -u -m pytest tests/test_gpu_derive.py tests/test_gpu_ga.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread -k "derive or derived or permutation or redo" ;;
