@@ -126,6 +126,16 @@ int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* 
 int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P, int max_steps,
                             double p1, double p2, double p3, const int32_t* order, void* stream);
 
+/* tt_local_search_ordered followed by the evaluation of every searched
+ * individual (localSearch, then computePenalty: ga.cpp:574-575), in the same
+ * launch: hcv, scv, penalty (i32) and feasible (u8) of individual i, as tt_eval
+ * would give them for the searched row (the -1 sentinels for an invalid genome,
+ * which the search leaves untouched). The four outputs are all given or all
+ * NULL (NULL: tt_local_search_ordered). */
+int tt_local_search_eval(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P, int max_steps,
+                         double p1, double p2, double p3, const int32_t* order, int32_t* hcv, int32_t* scv,
+                         uint8_t* feasible, int32_t* penalty, void* stream);
+
 /* Diagnostics: the step counts of the last tt_local_search call on `stream`
  * (waits for that call's counts, not for the whole stream): steps[0] = steps
  * taken in phase 2, steps[1] = all steps (0, 0 before any call on the stream

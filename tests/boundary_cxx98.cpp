@@ -75,6 +75,8 @@ int main() {
         bad += tt_lpt_order(NULL, NULL, 1, NULL, NULL, NULL) != TT_ERR_INVALID;
         bad += tt_local_search_stats(NULL, NULL, NULL) != TT_ERR_INVALID;
         bad += tt_local_search_masks(NULL, NULL, NULL) != TT_ERR_INVALID;
+        bad += tt_local_search_eval(NULL, NULL, NULL, NULL, 1, 200, 1.0, 1.0, 0.0, NULL, NULL, NULL, NULL, NULL, NULL) !=
+               TT_ERR_INVALID;
         bad += tt_ga_breed(NULL, NULL, NULL, NULL, 10, NULL, 1, 0.8, 0.5, 1, NULL, NULL, NULL, NULL) != TT_ERR_INVALID;
         bad += tt_ga_replace(NULL, NULL, NULL, NULL, NULL, NULL, NULL, 10, NULL, NULL, NULL, NULL, NULL, NULL, 1, NULL,
                              NULL) != TT_ERR_INVALID;

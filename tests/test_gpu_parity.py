@@ -541,3 +541,47 @@ def test_local_search_step_budget_windows(orc, dims, p1, p2):
             es, er, eg = o.local_search(start_s, start_r, seeds, steps, p1, p2)
             assert np.array_equal(host(s), es) and np.array_equal(host(r), er) and np.array_equal(host(g), eg), steps
     assert dp.status() == 0
+
+
+@pytest.mark.parametrize("dims,crowd,steps", [((50, 5, 4, 40), False, 300), ((400, 10, 5, 200), True, 400),
+                                              ((300, 12, 4, 150), False, 3000), ((449, 40, 5, 220), True, 300)],
+                         ids=["E50_small_path", "E400_redo", "E300_phase2", "E449R40_redo"])
+def test_local_search_eval_outputs_vs_eval(orc, dims, crowd, steps):
+    """tt_local_search_eval: the searched individuals' hcv, scv, feasible and
+    penalty computed at the end of the search launch (localSearch then
+    computePenalty, ga.cpp:574-575) equal tt_eval of the searched rows and the
+    oracle, on the one-launch path (E <= 64), through the redo launch
+    (crowded slots), into phase 2, with R > 16, and with an invalid genome
+    (left untouched, -1 sentinels); slots, rooms and RNG states equal
+    tt_local_search's."""
+    inst = ttga.generate(*dims, seed=47)
+    dp = native.DeviceProblem(inst)
+    o = orc.problem(inst)
+    P = 40
+    s0, r0, _ = o.random_init(ttga.population_seeds(4700, P))
+    if crowd:
+        rng = np.random.default_rng(2)
+        for k in range(1, P, 5):
+            s0[k, rng.choice(inst.E, size=int(rng.integers(65, 120)), replace=False)] = int(rng.integers(0, 45))
+        r0 = o.assign_rooms(s0)
+    s0[7, 3] = 45                                          # an invalid genome
+    seeds = ttga.population_seeds(4800, P)
+    s, r, g = dev(s0), dev(r0), dev(seeds)
+    out = (torch.empty(P, dtype=torch.int32, device="cuda"), torch.empty(P, dtype=torch.int32, device="cuda"),
+           torch.empty(P, dtype=torch.uint8, device="cuda"), torch.empty(P, dtype=torch.int32, device="cuda"))
+    dp.local_search(s, r, g, steps, out=out)
+    s2, r2, g2 = dev(s0), dev(r0), dev(seeds)
+    dp.local_search(s2, r2, g2, steps)
+    for a, b in zip((s, r, g), (s2, r2, g2)):
+        assert np.array_equal(host(a), host(b))
+    got = [host(t) for t in out]
+    ev = [host(t) for t in dp.eval(s, r)]
+    for x, e in zip(got, ev):
+        assert np.array_equal(x, e)
+    assert got[0][7] == -1 and got[3][7] == -1 and got[2][7] == 0
+    ok = np.arange(P) != 7
+    es, er, eg = o.local_search(s0[ok], r0[ok], seeds[ok], steps)
+    assert np.array_equal(host(s)[ok], es) and np.array_equal(host(r)[ok], er)
+    for x, e in zip(got, o.eval(es, er)):
+        assert np.array_equal(x[ok], e)
+    assert dp.status() == 2                                # bit 1: the invalid genome met by the search

@@ -88,6 +88,15 @@ __device__ __forceinline__ uint32_t pm_pow(int n) {
 // (int)(next() * n): truncation of the fp64 product (Solution.cpp:52, ga.cpp:135)
 __device__ __forceinline__ int pm_pick(int64_t& s, int n) { return (int)__dmul_rn(pm_next(s), (double)n); }
 
+// >2 in a row + single class of one student's attendance mask m, the 45-bit set
+// of slots the student attends (Solution.cpp:99-137)
+__device__ __forceinline__ int mask_scv(uint64_t m) {
+    int sc = __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);
+#pragma unroll
+    for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);
+    return sc;
+}
+
 // Full-wave sum (every lane active): DPP row shifts + readlane, no LDS round
 // trips. Written out rather than __reduce_add_sync, whose library reduction
 // also carries a partial-EXEC path at every call site (code size: the local

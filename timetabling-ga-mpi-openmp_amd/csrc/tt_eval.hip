@@ -217,13 +217,7 @@ __device__ __forceinline__ void keep_rec(const uint32_t (&r)[ST]) {
 // The lane phase over the size-sorted student lists (DevProblem::sid/srun):
 // a run holds `cnt` students of N ids each (N even, the last id may be the
 // sentinel E), so a student costs its own events plus at most one sentinel.
-// >2 in a row + single class of one student's attendance mask m (Solution.cpp:99-137)
-__device__ __forceinline__ int mask_scv(uint64_t m) {
-    int sc = __popcll(m & (m >> 1) & (m >> 2) & kTripleMask);
-#pragma unroll
-    for (int d = 0; d < 5; ++d) sc += (__popc((uint32_t)(m >> (9 * d)) & 0x1FFu) == 1);
-    return sc;
-}
+// mask_scv (>2 in a row + single class of one student's mask): tt_common.h
 // The same terms for a mask in the GAPPED slot layout of eval_lanes' tile
 // (TT_LANES_GAP): slot s = 9d + k sits at bit 10d + k for days 0-2 and at bit
 // 32 + 10(d - 3) + k for days 3-4, so every day is a 9-bit field followed by a

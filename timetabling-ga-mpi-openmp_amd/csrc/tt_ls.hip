@@ -1325,12 +1325,76 @@ __device__ __forceinline__ uint64_t refresh_hot(LsState& S, uint64_t hot, bool a
 // entries from redo_list[2], at most redo_cap of them: beyond that status bit
 // 4 is set) and its HBM row and stream are left as they were; NULL when no
 // task can overflow.
+// Optional evaluation of the searched individual (tt_local_search_eval): the
+// localSearch -> computePenalty pair of ga.cpp:574-575 in one launch, so a GA
+// generation needs no separate evaluation of its children after the search.
+struct LsEvalOut {
+    int32_t* hcv;
+    int32_t* scv;
+    uint8_t* feasible;
+    int32_t* penalty;
+};
+
+// computeFeasibility / computeHcv / computeScv / computePenalty
+// (Solution.cpp:63-170) of the individual in the wave's LDS state (slots sl,
+// rooms rr, slot bitsets B), in tt_eval.hip's closed forms:
+//   hcv = sum over (slot, room) cells of C(n, 2)          (:148-150)
+//       + #{i < j : same slot, correlated}                  (:151-153)
+//       + #{e : room not possible for e}                    (:155-156)
+//   scv = sum_e [slot_e % 9 == 8] studentNumber(e)          (:93-96)
+//       + sum over students of the >2-in-a-row and single-class terms of the
+//         student's slot mask                               (:99-137)
+// The room histogram is rebuilt from the rows (phase 2 keeps an owner table there).
+__device__ __forceinline__ void ls_eval(LsState& S, long p, const LsEvalOut& out) {
+    const DevProblem& pb = S.pb;
+    const int E = S.E, R = S.R, EW = S.EW, lane = S.lane;
+    for (int c = lane; c < kSlots * R; c += 64) S.hist[c] = 0;
+    wave_sync();
+    int h = 0, sc = 0;
+    if (lane < kSlots) {                                   // room clash pairs of slot `lane`
+        for (int w = 0; w < EW; ++w) {
+            uint64_t x = S.B[(size_t)lane * EW + w];
+            while (x) {
+                const int e = 64 * w + __builtin_ctzll(x);
+                x &= x - 1;
+                const int r = S.rr[e];
+                h += S.hist[lane * R + r];
+                S.hist[lane * R + r] = (uint16_t)(S.hist[lane * R + r] + 1);
+            }
+        }
+    }
+    int cp = 0;                                            // 2 x correlated pairs
+    for (int e = lane; e < E; e += 64) {
+        const int t = S.sl[e], r = S.rr[e];
+        for (int w = 0; w < EW; ++w) cp += __popcll(pb.corr64[(size_t)e * EW + w] & S.B[(size_t)t * EW + w]);
+        cp -= (int)((pb.corr64[(size_t)e * EW + (e >> 6)] >> (e & 63)) & 1ull);   // corr(e, e): e has a student
+        h += (int)(((pb.poss[e] >> r) & 1ull) ^ 1ull);
+        if ((kLastSlotMask >> t) & 1ull) sc += pb.sn[e];
+    }
+    for (int st = lane; st < pb.S; st += 64) {
+        uint64_t m = 0;
+        for (int k = pb.stu_off[st]; k < pb.stu_off[st + 1]; ++k) m |= 1ull << S.sl[pb.stu_ev[k]];
+        sc += mask_scv(m);
+    }
+    h = wave_sum(h);
+    cp = wave_sum(cp);
+    sc = wave_sum(sc);
+    if (lane == 0) {
+        const int hcv = h + cp / 2;
+        out.hcv[p] = hcv;
+        out.scv[p] = sc;
+        out.feasible[p] = hcv == 0 ? 1 : 0;
+        out.penalty[p] = hcv == 0 ? sc : 1000000 + hcv;
+    }
+}
+
 template <int CAP>
 __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& pb, uint8_t* __restrict__ slot,
                                                              uint8_t* __restrict__ room, int64_t* __restrict__ rng,
                                                              long p, int max_steps, double p1, double p2, double p3,
                                                              int32_t* __restrict__ redo_list, int redo_cap, int smS,
-                                                             unsigned long long* __restrict__ ph_steps) {
+                                                             unsigned long long* __restrict__ ph_steps,
+                                                             const LsEvalOut& eout) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int E = pb.E, R = pb.R, EW = pb.EW64;
     const int lane = threadIdx.x;
@@ -1382,7 +1446,12 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
     for (int c = lane; c < kSlots * R; c += 64) S.hist[c] = 0;
     __syncthreads();
     if (wave_any(bad)) {                       // invalid genome: leave it untouched
-        if (lane == 0) atomicOr(pb.status, 2);
+        if (lane == 0) {
+            atomicOr(pb.status, 2);
+            if (eout.hcv) {                    // tt_eval's sentinels for an invalid genome
+                eout.hcv[p] = -1; eout.scv[p] = -1; eout.feasible[p] = 0; eout.penalty[p] = -1;
+            }
+        }
         return;
     }
     for (int e = lane; e < E; e += 64) {
@@ -1705,6 +1774,7 @@ __device__ __attribute__((always_inline)) inline void ls_one(const DevProblem& p
         room[p * E + e] = S.rr[e];
     }
     if (lane == 0) rng[p] = st;
+    if (eout.hcv) ls_eval(S, p, eout);
 #ifdef TT_LS_PROF
     LSP_ADD(S, kPfTotal, t_kernel);
     LSP_CNT(S, kPfWaves);
@@ -1740,10 +1810,10 @@ template <int CAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE))) void local_search_kernel(
     DevProblem pb, uint8_t* __restrict__ slot, uint8_t* __restrict__ room, int64_t* __restrict__ rng, int P,
     int max_steps, double p1, double p2, double p3, int32_t* __restrict__ redo_list, int redo_cap,
-    const int32_t* __restrict__ order, int smS, unsigned long long* __restrict__ ph_steps) {
+    const int32_t* __restrict__ order, int smS, unsigned long long* __restrict__ ph_steps, LsEvalOut eout) {
     const long p = order ? (long)order[blockIdx.x] : (long)blockIdx.x;   // dispatch order only
     if ((unsigned long)p >= (unsigned long)P) return;
-    ls_one<CAP>(pb, slot, room, rng, p, max_steps, p1, p2, p3, redo_list, redo_cap, smS, ph_steps);
+    ls_one<CAP>(pb, slot, room, rng, p, max_steps, p1, p2, p3, redo_list, redo_cap, smS, ph_steps, eout);
 }
 
 // Redo launch: a grid of resident waves works through the individuals the
@@ -1754,13 +1824,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE)))
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TT_LS_WPE))) void local_search_redo_kernel(
     DevProblem pb, uint8_t* __restrict__ slot, uint8_t* __restrict__ room, int64_t* __restrict__ rng, int max_steps,
     double p1, double p2, double p3, int32_t* __restrict__ redo_list, int redo_cap, int smS,
-    unsigned long long* __restrict__ ph_steps) {
+    unsigned long long* __restrict__ ph_steps, LsEvalOut eout) {
     const int n = min(redo_list[0], redo_cap);
     if (n == 0) return;             // nothing listed: every wave sees 0, no reset needed (no arrival atomics)
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         __syncthreads();
         ls_one<kMaxSlotEvents>(pb, slot, room, rng, (long)redo_list[2 + i], max_steps, p1, p2, p3, nullptr, 0, smS,
-                               ph_steps);
+                               ph_steps, eout);
     }
     __threadfence();
     if (threadIdx.x == 0 && atomicAdd(&redo_list[1], 1) == (int)gridDim.x - 1) {
@@ -1917,9 +1987,19 @@ extern "C" int tt_local_search(const tt_problem* p, uint8_t* slot, uint8_t* room
 extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P,
                                        int max_steps, double p1, double p2, double p3, const int32_t* order,
                                        void* stream) {
+    return tt_local_search_eval(p, slot, room, rng, P, max_steps, p1, p2, p3, order, nullptr, nullptr, nullptr,
+                                nullptr, stream);
+}
+
+extern "C" int tt_local_search_eval(const tt_problem* p, uint8_t* slot, uint8_t* room, int64_t* rng, int P,
+                                    int max_steps, double p1, double p2, double p3, const int32_t* order,
+                                    int32_t* hcv, int32_t* scv, uint8_t* feasible, int32_t* penalty, void* stream) {
     int rc = check_pop_args(p, P, slot, room);
     if (rc || P == 0) return rc;
     if (!rng) { set_error("null rng buffer"); return TT_ERR_INVALID; }
+    const int nout = (hcv != nullptr) + (scv != nullptr) + (feasible != nullptr) + (penalty != nullptr);
+    if (nout != 0 && nout != 4) { set_error("evaluation outputs: all four or none"); return TT_ERR_INVALID; }
+    const LsEvalOut eout{hcv, scv, feasible, penalty};
     if (max_steps < 0) { set_error("negative max_steps"); return TT_ERR_INVALID; }
     if ((rc = use_device(p))) return rc;
     const int smf = ls_mask_students(p, kMaxSlotEvents, local_search_kernel<kMaxSlotEvents>, P);
@@ -1935,7 +2015,7 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
     if (p->E <= kLsCapSmall) {                      // no slot can exceed the small tasks
         hipLaunchKernelGGL(local_search_kernel<kMaxSlotEvents>, dim3(P), dim3(64), Lf.bytes, st, p->dev, slot, room,
                            rng, P, max_steps, p1, p2, p3, (int32_t*)nullptr, 0, order, smf,
-                           (unsigned long long*)nullptr);
+                           (unsigned long long*)nullptr, eout);
         return check_hip(hipGetLastError(), "local_search launch");
     }
     tt_problem* mp = const_cast<tt_problem*>(p);
@@ -1984,7 +2064,7 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
         rl->cap = P;
     }
     hipLaunchKernelGGL(local_search_kernel<kLsCapSmall>, dim3(P), dim3(64), Ls.bytes, st, p->dev, slot, room, rng, P,
-                       max_steps, p1, p2, p3, rl->list, rl->cap, order, sms, rl->ph_dev);
+                       max_steps, p1, p2, p3, rl->list, rl->cap, order, sms, rl->ph_dev, eout);
     TT_HIP(hipGetLastError());
     // the redo launch: resident waves only (an empty list costs one short launch)
     int per_cu = 0;
@@ -1995,7 +2075,7 @@ extern "C" int tt_local_search_ordered(const tt_problem* p, uint8_t* slot, uint8
     per_cu = std::min(per_cu, lds_resident_limit(Lf.bytes));
     const int grid = std::min(P, std::max(1, per_cu) * p->num_cus);
     hipLaunchKernelGGL(local_search_redo_kernel, dim3(grid), dim3(64), Lf.bytes, st, p->dev, slot, room, rng,
-                       max_steps, p1, p2, p3, rl->list, rl->cap, smf, rl->ph_dev);
+                       max_steps, p1, p2, p3, rl->list, rl->cap, smf, rl->ph_dev, eout);
     const hipError_t he = hipGetLastError();
     if (he != hipSuccess) {
         // the first launch may have listed individuals: leave the list empty

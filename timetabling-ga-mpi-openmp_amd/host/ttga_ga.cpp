@@ -467,8 +467,9 @@ struct Island {
     // ga.cpp:429-434 for every member, then the population is sorted
     void initialize() {
         check_tt(tt_random_init(tp, rng_init, pop.slot, pop.room, N, st), "tt_random_init");
-        check_tt(tt_local_search(tp, pop.slot, pop.room, rng_init, N, max_steps, p1, p2, p3, st), "tt_local_search");
-        evaluate(pop);
+        check_tt(tt_local_search_eval(tp, pop.slot, pop.room, rng_init, N, max_steps, p1, p2, p3, nullptr, pop.hcv,
+                                      pop.scv, pop.feasible, pop.penalty, st),
+                 "tt_local_search_eval");
         check_tt(tt_ga_replace(tp, pop.slot, pop.room, pop.hcv, pop.scv, pop.feasible, pop.penalty, N, pop.slot,
                                pop.room, pop.hcv, pop.scv, pop.feasible, pop.penalty, 0, work, st),
                  "tt_ga_replace");
@@ -494,21 +495,20 @@ struct Island {
     }
 
     // LPT order (C >= kLptMinChildren), localSearch and evaluation of rows [off, off + n) on s
+    // (the search and the evaluation in one launch: ga.cpp:574-575)
     void search(int off, int n, hipStream_t s, void* w) {
         Pop c = child_rows(off, n);
+        const int32_t* ord = nullptr;
         if (order) {
             // longest-expected first: the children's hcv before the search, descending
             // (a generation's search launch ends with its slowest children); same results
             evaluate(c, s);
             check_tt(tt_lpt_order(tp, c.hcv, n, order + off, w, s), "tt_lpt_order");
-            check_tt(tt_local_search_ordered(tp, c.slot, c.room, rng_child + off, n, max_steps, p1, p2, p3, order + off,
-                                             s),
-                     "tt_local_search_ordered");
-        } else {
-            check_tt(tt_local_search(tp, c.slot, c.room, rng_child + off, n, max_steps, p1, p2, p3, s),
-                     "tt_local_search");
+            ord = order + off;
         }
-        evaluate(c, s);
+        check_tt(tt_local_search_eval(tp, c.slot, c.room, rng_child + off, n, max_steps, p1, p2, p3, ord, c.hcv, c.scv,
+                                      c.feasible, c.penalty, s),
+                 "tt_local_search_eval");
     }
 
     void replace(int off, int n, hipStream_t s, void* w) {

@@ -24,7 +24,7 @@ EXPORTS = (
     "tt_eval_variant", "tt_assign_rooms", "tt_random_init", "tt_crossover", "tt_mutation", "tt_local_search",
     "tt_device_status", "tt_last_error", "tt_version", "tt_ga_breed", "tt_ga_work_bytes", "tt_ga_replace",
     "tt_eval_auto_variant", "tt_local_search_ordered", "tt_lpt_order", "tt_ga_work_source_offset",
-    "tt_local_search_stats", "tt_local_search_masks",
+    "tt_local_search_stats", "tt_local_search_masks", "tt_local_search_eval",
 )
 
 _lib = None
@@ -62,6 +62,7 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.tt_lpt_order.argtypes = [vp, vp, i32, vp, vp, vp]
     lib.tt_local_search_stats.argtypes = [vp, vp, vp]
     lib.tt_local_search_masks.argtypes = [vp, vp, vp]
+    lib.tt_local_search_eval.argtypes = [vp, vp, vp, vp, i32, i32, dbl, dbl, dbl, vp, vp, vp, vp, vp, vp]
     lib.tt_device_status.argtypes = [vp, vp]
     lib.tt_eval_auto_variant.argtypes = [vp]
     lib.tt_ga_breed.argtypes = [vp, vp, vp, vp, i32, vp, i32, dbl, dbl, i32, vp, vp, vp, vp]
@@ -191,11 +192,26 @@ class DeviceProblem:
         _check(self.lib, self.lib.tt_mutation(self.handle, slot.data_ptr(), room.data_ptr(), rng.data_ptr(), P,
                                               self._stream(slot)))
 
-    def local_search(self, slot, room, rng, max_steps: int, p1=1.0, p2=1.0, p3=0.0, order=None):
-        """order: optional int32 device permutation, the dispatch order (results unchanged)."""
+    def local_search(self, slot, room, rng, max_steps: int, p1=1.0, p2=1.0, p3=0.0, order=None, out=None):
+        """order: optional int32 device permutation, the dispatch order (results unchanged).
+        out: optional (hcv, scv, feasible, penalty) device tensors of P entries, filled with
+        the searched individuals' evaluation in the same launch (tt_local_search_eval)."""
         import torch
         P = self._pop(slot, room)
         self._rng(rng, P)
+        if out is not None:
+            if order is not None and not (order.is_cuda and order.dtype == torch.int32 and order.is_contiguous()
+                                          and order.numel() == P):
+                raise ValueError("order must be a contiguous int32 CUDA tensor of P entries")
+            hcv, scv, feas, pen = out
+            for t, dt in ((hcv, torch.int32), (scv, torch.int32), (feas, torch.uint8), (pen, torch.int32)):
+                if not (t.is_cuda and t.dtype == dt and t.is_contiguous() and t.numel() == P):
+                    raise ValueError("out must be contiguous CUDA tensors (int32, int32, uint8, int32) of P entries")
+            _check(self.lib, self.lib.tt_local_search_eval(
+                self.handle, slot.data_ptr(), room.data_ptr(), rng.data_ptr(), P, int(max_steps), float(p1),
+                float(p2), float(p3), ctypes.c_void_p(order.data_ptr() if order is not None else None),
+                hcv.data_ptr(), scv.data_ptr(), feas.data_ptr(), pen.data_ptr(), self._stream(slot)))
+            return
         if order is None:
             _check(self.lib, self.lib.tt_local_search(self.handle, slot.data_ptr(), room.data_ptr(), rng.data_ptr(),
                                                       P, int(max_steps), float(p1), float(p2), float(p3),
