@@ -205,6 +205,11 @@ class Island(Members):
         self.rng_child = torch.from_numpy(stream_seeds(seed, self.N, self.C)).to(dev)
         self.work = dp.ga_work(self.N)
         self.generation = 0
+        if schedule == "staggered" and stream is None:
+            # every part on a stream of its own, the first included: work on the legacy
+            # null stream orders itself against the other streams' work, which would
+            # serialise the parts (profiles/r06_n_trace_overlap_comp20_staggered.json)
+            stream = _side_streams(dev, None, 1)[0]
         self.stream = stream
         self.schedule = schedule
         self.parts = int(parts) if schedule == "staggered" else 1
@@ -287,8 +292,8 @@ class Island(Members):
         with self._on_stream():
             p = self.pop
             self.dp.random_init(self.rng_init, p["slot"], p["room"])
-            self.dp.local_search(p["slot"], p["room"], self.rng_init, self.max_steps, self.p1, self.p2, self.p3)
-            self._evaluate(p)
+            self.dp.local_search(p["slot"], p["room"], self.rng_init, self.max_steps, self.p1, self.p2, self.p3,
+                                 out=(p["hcv"], p["scv"], p["feasible"], p["penalty"]))
             self.dp.ga_replace(p, None, self.work)
             if self.schedule == "staggered":
                 self._ev_op.record()
@@ -305,15 +310,16 @@ class Island(Members):
             self._step()
 
     def _search(self, c, rng, work):
-        """LPT order (optional), localSearch and evaluation of children c."""
+        """LPT order (optional), localSearch and evaluation of children c (one
+        launch: tt_local_search_eval, ga.cpp:574-575)."""
         order = None
         if self.lpt:
             # dispatch the children longest-expected first (hcv before the search,
             # descending): the launch's tail is its slowest waves; results unchanged
             self._evaluate(c)
             order = self.dp.lpt_order(c["hcv"], work)
-        self.dp.local_search(c["slot"], c["room"], rng, self.max_steps, self.p1, self.p2, self.p3, order=order)
-        self._evaluate(c)
+        self.dp.local_search(c["slot"], c["room"], rng, self.max_steps, self.p1, self.p2, self.p3, order=order,
+                             out=(c["hcv"], c["scv"], c["feasible"], c["penalty"]))
 
     def _step(self):
         c = self.child
