@@ -167,6 +167,37 @@ def test_island_staggered_vs_oracle(sm, N, C, gens, lpt, reads, parts):
     assert np.all(np.diff(pop["penalty"].astype(np.uint32)) >= 0)
 
 
+def test_island_staggered_orders_the_callers_stream():
+    """Island(stream=None, schedule="staggered") runs its parts on streams of
+    their own; the caller's work on torch's current stream must still see the
+    population as the last step left it (what tools/ga_quality.py's per-
+    generation log does): clones taken on the current stream right after each
+    step, with no host sync, equal those of a twin island read after a full
+    device sync; pop[0]'s penalty never rises."""
+    inst = ttga.config_instance("comp01")
+    dp = native.DeviceProblem(inst)
+    N, C, gens, steps, seed = 256, 128, 6, 1000, 11
+    logs = []
+    for synced in (False, True):
+        isl = Island(dp, pop_size=N, children=C, max_steps=steps, seed=seed, lpt=True, schedule="staggered")
+        isl.initialize()
+        got = []
+        for _ in range(gens):
+            isl.step()
+            if synced:
+                torch.cuda.synchronize()
+            got.append(torch.stack([isl.pop["penalty"].clone(), isl.pop["scv"].clone()]))
+        isl.flush()
+        got.append(torch.stack([isl.pop["penalty"].clone(), isl.pop["scv"].clone()]))
+        torch.cuda.synchronize()
+        logs.append([host(t) for t in got])
+        isl.close()
+    for g, (a, b) in enumerate(zip(*logs)):
+        assert np.array_equal(a, b), g
+    best = np.array([t[0, 0] for t in logs[0]]).astype(np.uint32).astype(np.int64)    # -1 sentinel: last
+    assert np.all(np.diff(best) <= 0), best
+
+
 def test_island_staggered_comp01_vs_oracle():
     """The staggered schedule on a comp01-size instance (the GA bench's
     configs[2] shape): 512 members, 256 children per generation (LPT on), four

@@ -365,20 +365,8 @@ __device__ __forceinline__ void scv_terms(LsState& S, int e, bool nb, int& es, i
 #ifndef TT_LS_WLT
 #define TT_LS_WLT 1
 #endif
-// lane j of (lo, hi) = the 64-bit wave-uniform v. The lane select goes
-// through M0 (gfx9 reads one SGPR per VALU instruction besides M0); the s_nop
-// pads the M0 write (inline asm gets no hazard padding from the compiler).
-// Nothing else in the local-search kernel uses M0 (no LDS-DMA, no movrel), so
-// clobbering it is safe; clang warns that M0 is reserved.
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void writelane64(uint32_t& lo, uint32_t& hi, uint64_t v, int j) {
-    asm volatile("s_mov_b32 m0, %4\n\ts_nop 1\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
-                 : "+v"(lo), "+v"(hi)
-                 : "s"((uint32_t)v), "s"((uint32_t)(v >> 32)), "s"(j)
-                 : "m0");
-}
-#pragma clang diagnostic pop
+// (writelane64 is in tt_match.h; nothing else in the local-search kernel uses
+// M0 -- no LDS-DMA, no movrel.)
 
 // Wave matcher for one touched slot of N <= 64 events, the same search as
 // match_slot<1> (tt_match.h, Solution.cpp:772-891), with its state in

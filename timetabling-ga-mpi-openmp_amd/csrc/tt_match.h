@@ -25,31 +25,54 @@ constexpr uint8_t kNone = 0xFF;
 #define TT_BUCKETS_CHUNK 1
 #endif
 
-// Per-wave LDS scratch for one individual.
+// TT_ROOMS_WAVE: assign_touched matches a slot by the whole wave
+// (wave_match_slot) instead of one slot per lane (match_slot / match_slot_reg:
+// lane-serial searches that wait on LDS at every step), except the many small
+// slots of a whole-row assignment on an instance of <= 16 rooms, which stay one
+// per lane in registers; slots of more than 64 events stay lane-serial.
+#ifndef TT_ROOMS_WAVE
+#define TT_ROOMS_WAVE 1
+#endif
+constexpr int kWaveSlots = 8;    // touched slots up to which every slot goes to the wave matcher
+
+// Per-wave LDS scratch for one individual. Two layouts:
+//  * R <= 16 (or TT_ROOMS_WAVE=0): every slot's possible-room masks, matched
+//    rooms, room owners and dads, for one slot per lane;
+//  * R > 16 ("wide", TT_ROOMS_WAVE): the wave matcher keeps its state in
+//    registers and reads the possible rooms from the problem (L2-resident), so
+//    the scratch holds the row, its buckets and one crowded slot's state for
+//    the lane-serial fallback: 4E + 2.4 KB instead of 14E + 90R (syn: 11 KB
+//    instead of 30 KB, 14 instead of 5 waves per CU).
 struct MatchScratch {
     uint8_t* sl;        // [E]     slot of each event
     uint8_t* rr;        // [E]     room of each event (output row)
     uint16_t* bev;      // [E]     events bucketed by slot, ascending inside a slot
-    uint8_t* mr;        // [E]     matched room per bucket position (kNone)
-    uint64_t* pl;       // [E]     possible-room mask per bucket position
-    uint8_t* rm;        // [45*R]  event (bucket-local index) matched to each room
-    uint8_t* dr;        // [45*R]  dad (bucket-local event) of each room in the search
+    uint8_t* mr;        // [E]     matched room per bucket position (kNone)   wide: [256], one slot
+    uint64_t* pl;       // [E]     possible-room mask per bucket position    wide: [256], one slot
+    uint8_t* rm;        // [45*R]  event (bucket-local index) matched to each room   wide: [R]
+    uint8_t* dr;        // [45*R]  dad (bucket-local event) of each room in the search   wide: [R]
     int32_t* bstart;    // [46]    bucket offsets
     uint32_t* tmp;      // [64]
     uint32_t* flags;    // [4]
     uint64_t* cm;       // [64]    per-slot lane masks of one 64-event chunk (build_buckets)
+    bool wide;
 };
 
+__host__ __device__ inline bool match_wide(int R) { return TT_ROOMS_WAVE && R > 16; }
+
 __host__ __device__ inline size_t match_scratch_bytes(int E, int R) {
+    const bool wide = match_wide(R);
+    const size_t nb = wide ? (size_t)kMaxSlotEvents : (size_t)E;     // bucket positions with state
+    const size_t nr = wide ? (size_t)R : (size_t)kSlots * R;
     size_t b = 0;
     b += (size_t)E;                          // sl
     b += (size_t)E;                          // rr
     b = (b + 1) & ~(size_t)1;
     b += 2 * (size_t)E;                      // bev
-    b += (size_t)E;                          // mr
+    b += nb;                                 // mr
     b = (b + 7) & ~(size_t)7;
-    b += 8 * (size_t)E;                      // pl
-    b += 2 * (size_t)kSlots * R;             // rm, dr
+    b += 8 * nb;                             // pl
+    b += 2 * nr;                             // rm, dr
     b = (b + 3) & ~(size_t)3;
     b += 4 * 46 + 4 * 64 + 4 * 4;            // bstart, tmp, flags
     b = (b + 7) & ~(size_t)7;
@@ -59,16 +82,19 @@ __host__ __device__ inline size_t match_scratch_bytes(int E, int R) {
 
 __device__ inline MatchScratch carve_match_scratch(uint8_t* base, int E, int R) {
     MatchScratch m;
+    m.wide = match_wide(R);
+    const size_t nb = m.wide ? (size_t)kMaxSlotEvents : (size_t)E;
+    const size_t nr = m.wide ? (size_t)R : (size_t)kSlots * R;
     size_t b = 0;
     m.sl = base + b; b += E;
     m.rr = base + b; b += E;
     b = (b + 1) & ~(size_t)1;
     m.bev = (uint16_t*)(base + b); b += 2 * (size_t)E;
-    m.mr = base + b; b += E;
+    m.mr = base + b; b += nb;
     b = (b + 7) & ~(size_t)7;
-    m.pl = (uint64_t*)(base + b); b += 8 * (size_t)E;
-    m.rm = base + b; b += (size_t)kSlots * R;
-    m.dr = base + b; b += (size_t)kSlots * R;
+    m.pl = (uint64_t*)(base + b); b += 8 * nb;
+    m.rm = base + b; b += nr;
+    m.dr = base + b; b += nr;
     b = (b + 3) & ~(size_t)3;
     m.bstart = (int32_t*)(base + b); b += 4 * 46;
     m.tmp = (uint32_t*)(base + b); b += 4 * 64;
@@ -141,6 +167,7 @@ __device__ inline void build_buckets(const DevProblem& pb, MatchScratch& m, int 
         if (m.sl[e] == me) m.bev[pos++] = (uint16_t)e;
 #endif
     __syncthreads();
+    if (m.wide) return;                                // the wave matcher reads pb.poss itself
     const int nb = m.bstart[kSlots];
     for (int b0 = 0; b0 < nb; b0 += 512) {            // eight gathers in flight per block
         uint64_t v[8];
@@ -355,10 +382,162 @@ __device__ void match_slot_reg(const uint16_t* ev, const uint64_t* pl, int N, ui
     }
 }
 
+// lane j of (lo, hi) = the 64-bit wave-uniform v. The lane select goes
+// through M0 (gfx9 reads one SGPR per VALU instruction besides M0); the s_nop
+// pads the M0 write (inline asm gets no hazard padding from the compiler).
+// M0 is declared clobbered; no kernel that calls this uses LDS-DMA or movrel.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void writelane64(uint32_t& lo, uint32_t& hi, uint64_t v, int j) {
+    asm volatile("s_mov_b32 m0, %4\n\ts_nop 1\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
+                 : "+v"(lo), "+v"(hi)
+                 : "s"((uint32_t)v), "s"((uint32_t)(v >> 32)), "s"(j)
+                 : "m0");
+}
+#pragma clang diagnostic pop
+
+// One slot of N <= 64 events matched by the whole wave (the local search's
+// match_task_wave without its bookkeeping): lane i holds event i's possible
+// rooms pl (zero past N) and matched room mr; lane j holds room j's matched
+// event rm, its possible rooms plr, its search dad dr, and the events that may
+// use it (eor); the seen / fringe room sets are wave-uniform bitsets. Same
+// search and read-out as match_slot (Solution.cpp:802-891):
+//  * the search expands every fringe event before any room, so its first
+//    stage (all unmatched events, ascending) is closed-form: the rooms seen are
+//    those with an unmatched candidate, room j's dad its lowest one;
+//  * the room stage pops fringe rooms ascending; a matched room's event is
+//    expanded at once and can only discover unseen rooms, so every popped room
+//    whose event discovers none is popped in bulk (one ballot), up to the
+//    first that does or the lowest free room (the sink).
+// Returns event lane's room (lanes < N).
+__device__ __forceinline__ uint32_t wave_match_slot(int R, int N, uint64_t pl, int lane) {
+    constexpr uint32_t NONE = 0xFFu;
+    const uint32_t pl_lo = (uint32_t)pl, pl_hi = (uint32_t)(pl >> 32);
+    uint32_t eor_lo = 0, eor_hi = 0;
+    const int r1 = R < 32 ? R : 32;
+    for (int j = 0; j < r1; ++j) writelane64(eor_lo, eor_hi, ballot((pl_lo >> j) & 1u), j);
+    for (int j = 32; j < R; ++j) writelane64(eor_lo, eor_hi, ballot((pl_hi >> (j - 32)) & 1u), j);
+    const uint64_t eor = ((uint64_t)eor_hi << 32) | eor_lo;
+    uint32_t mr = NONE, rm = 0, dr = 0, plr_lo = 0, plr_hi = 0;
+    uint64_t unm = N >= 64 ? ~0ull : ((1ull << N) - 1ull);
+    uint64_t rmatched = 0;
+    for (;;) {
+        const uint64_t cand = eor & unm;                 // stage 1, closed form
+        uint64_t sr = ballot(cand != 0ull), fr = sr;     // eor is zero on lanes >= R
+        if (cand) dr = (uint32_t)__builtin_ctzll(cand);
+        int sink = -1;
+        for (;;) {                                       // stage 2, bulk pops
+            const uint64_t freef = fr & ~rmatched;
+            const uint64_t M = fr & (freef ? (freef & (0ull - freef)) - 1ull : ~0ull);
+            const uint64_t plr = ((uint64_t)plr_hi << 32) | plr_lo;
+            const uint64_t disc = ballot(((M >> lane) & 1ull) && (plr & ~sr) != 0ull);
+            if (!disc) {
+                if (freef) sink = __builtin_ctzll(freef);
+                break;
+            }
+            const int j = __builtin_ctzll(disc);
+            fr &= ~(M & ((2ull << j) - 1ull));           // pops M's rooms up to j
+            const int i2 = __builtin_amdgcn_readlane((int)rm, j);
+            const uint64_t pli = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)plr_hi, j) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)plr_lo, j);
+            const uint64_t nr = pli & ~sr;
+            sr |= nr;
+            fr |= nr;
+            if ((nr >> lane) & 1ull) dr = (uint32_t)i2;
+        }
+        if (sink < 0) break;
+        int j = sink;                                    // maxMatching augmentation (Solution.cpp:836-849)
+        for (;;) {
+            const int i = __builtin_amdgcn_readlane((int)dr, j);
+            const uint32_t prev = (uint32_t)__builtin_amdgcn_readlane((int)mr, i);
+            const uint32_t pi_lo = (uint32_t)__builtin_amdgcn_readlane((int)pl_lo, i);
+            const uint32_t pi_hi = (uint32_t)__builtin_amdgcn_readlane((int)pl_hi, i);
+            if (lane == i) mr = (uint32_t)j;
+            if (lane == j) { rm = (uint32_t)i; plr_lo = pi_lo; plr_hi = pi_hi; }
+            rmatched |= 1ull << j;
+            if (prev == NONE) { unm &= ~(1ull << i); break; }
+            j = (int)prev;
+        }
+    }
+    // read-out (Solution.cpp:802-830): unplaced events, ascending, take the first
+    // free possible room, else the first possible room; one with no possible room
+    // keeps lessBusy carried over from the previous unplaced event (initially 0)
+    const bool un = lane < N && mr == NONE;
+    if (!ballot(un)) return mr;
+    uint32_t v = 0;
+    if (un && pl) {
+        v = (uint32_t)__builtin_ctzll(pl);
+        if ((rmatched >> v) & 1ull) {
+            const uint64_t fr2 = pl & ~rmatched;
+            if (fr2) v = (uint32_t)__builtin_ctzll(fr2);
+        }
+    }
+    const uint64_t carriers = ballot(un && pl != 0ull);
+    const uint64_t below = carriers & ((1ull << lane) - 1ull);
+    const int src = below ? 63 - __builtin_clzll(below) : lane;
+    const uint32_t carried = (uint32_t)__shfl((int)v, src, 64);
+    return !un ? mr : (pl ? v : (below ? carried : 0u));
+}
+
 // Re-assign rooms for every slot t with bit t of `touched` set and a
 // non-empty bucket. m.sl and m.rr hold the individual's row; rooms of
 // untouched slots in m.rr are left as they are. Buckets must be built.
 __device__ inline void assign_touched(const DevProblem& pb, MatchScratch& m, uint64_t touched, int lane) {
+#if TT_ROOMS_WAVE
+    const int R = pb.R;
+    touched &= (1ull << kSlots) - 1ull;
+    if (!m.wide && __popcll(touched) > kWaveSlots) {
+        // a whole row on a small instance: slots of <= 32 events one per lane, in
+        // registers, all at once; the crowded ones go to the wave below
+        bool mine = false;
+        if (lane < kSlots && ((touched >> lane) & 1ull)) {
+            const int b0 = m.bstart[lane];
+            const int N = m.bstart[lane + 1] - b0;
+            if (N <= 32) {
+                mine = true;
+                if (N > 0) match_slot_reg(m.bev + b0, m.pl + b0, N, m.dr + lane * R, m.rr);
+            }
+        }
+        touched &= ~ballot(mine);
+    }
+    // the wave's slots one after another; the next slot's events and possible
+    // rooms are loaded while the current one is matched
+    int t = touched ? __builtin_ctzll(touched) : 0;
+    int b0 = __builtin_amdgcn_readfirstlane(m.bstart[t]);
+    int N = __builtin_amdgcn_readfirstlane(m.bstart[t + 1]) - b0;
+    int ev = lane < N ? m.bev[b0 + lane] : 0;
+    uint64_t pl = lane < N && N <= 64 ? (m.wide ? pb.poss[ev] : m.pl[b0 + lane]) : 0ull;
+    while (touched) {
+        touched &= touched - 1;
+        const int tc = t, bc = b0, Nc = N, evc = ev;
+        const uint64_t plc = pl;
+        if (touched) {
+            t = __builtin_ctzll(touched);
+            b0 = __builtin_amdgcn_readfirstlane(m.bstart[t]);
+            N = __builtin_amdgcn_readfirstlane(m.bstart[t + 1]) - b0;
+            ev = lane < N ? m.bev[b0 + lane] : 0;
+            pl = lane < N && N <= 64 ? (m.wide ? pb.poss[ev] : m.pl[b0 + lane]) : 0ull;
+        }
+        if (Nc == 0) continue;
+        if (Nc <= 64) {
+            const uint32_t r = wave_match_slot(R, Nc, plc, lane);
+            if (lane < Nc) m.rr[evc] = (uint8_t)r;
+        } else if (Nc <= kMaxSlotEvents) {
+            uint64_t* spl = m.wide ? m.pl : m.pl + bc;                     // the wide layout: one slot's state
+            uint8_t* smr = m.wide ? m.mr : m.mr + bc;
+            uint8_t* srm = m.wide ? m.rm : m.rm + tc * R;
+            uint8_t* sdr = m.wide ? m.dr : m.dr + tc * R;
+            if (m.wide)
+                for (int i = lane; i < Nc; i += 64) spl[i] = pb.poss[m.bev[bc + i]];
+            __syncthreads();
+            if (lane == 0) match_slot<4>(R, m.bev + bc, spl, Nc, smr, srm, sdr, m.rr);
+            __syncthreads();
+        } else {
+            for (int i = lane; i < Nc; i += 64) m.rr[m.bev[bc + i]] = 0xFF;
+            if (lane == 0) atomicOr(pb.status, 1);
+        }
+    }
+#else
     if (lane < kSlots && ((touched >> lane) & 1ull)) {
         const int b0 = m.bstart[lane];
         const int N = m.bstart[lane + 1] - b0;
@@ -376,6 +555,7 @@ __device__ inline void assign_touched(const DevProblem& pb, MatchScratch& m, uin
             }
         }
     }
+#endif
     __syncthreads();
 }
 

@@ -170,7 +170,12 @@ class Island(Members):
     population while the other threads' children are still searched. step()
     advances `parts` sub-batches and leaves parts - 1 of them pending; flush()
     replaces them (every host read of the population flushes first; the
-    snapshots the drivers log from do not).
+    snapshots the drivers log from do not). The parts run on streams of their
+    own even when the island's stream is None; initialize(), step() and
+    flush() order their population operations after the caller's work on its
+    stream (the island's, else torch's current stream) and make that stream
+    wait for the last of them, so the caller's next reads and writes of the
+    population are ordered as on a batch island.
     """
 
     def __init__(self, dp, pop_size: int = 10, children: int = 1, max_steps: int = 200, seed: int = 1,
@@ -205,6 +210,7 @@ class Island(Members):
         self.rng_child = torch.from_numpy(stream_seeds(seed, self.N, self.C)).to(dev)
         self.work = dp.ga_work(self.N)
         self.generation = 0
+        self._user_stream = stream                    # None: torch's current stream at each call
         if schedule == "staggered" and stream is None:
             # every part on a stream of its own, the first included: work on the legacy
             # null stream orders itself against the other streams' work, which would
@@ -259,6 +265,29 @@ class Island(Members):
             st.synchronize()
         torch.cuda.current_stream(self.pop["slot"].device).synchronize()
 
+    def _base(self):
+        """The stream the caller orders its own work on: the island's stream as
+        given, else torch's current stream."""
+        import torch
+        return (self._user_stream if self._user_stream is not None
+                else torch.cuda.current_stream(self.pop["slot"].device))
+
+    def _fork(self):
+        """Staggered: the population operations enqueued next come after the
+        caller's work enqueued so far on _base() (the chain's event takes it in)."""
+        s0 = self._streams[0]
+        b = self._base()
+        if b != s0:
+            s0.wait_stream(b)
+        s0.wait_event(self._ev_op)
+        self._ev_op.record(s0)
+
+    def _join(self):
+        """Staggered: the caller's stream (_base()) waits for the population's
+        last operation, so what it enqueues next sees the population as a batch
+        schedule on that stream would leave it (pending sub-batches aside)."""
+        self._base().wait_event(self._ev_op)
+
     def _on_stream(self, stream=None):
         import contextlib
 
@@ -289,6 +318,8 @@ class Island(Members):
 
     def initialize(self):
         """ga.cpp:429-434 for every member, then the population is sorted."""
+        if self.schedule == "staggered":
+            self._fork()
         with self._on_stream():
             p = self.pop
             self.dp.random_init(self.rng_init, p["slot"], p["room"])
@@ -297,13 +328,17 @@ class Island(Members):
             self.dp.ga_replace(p, None, self.work)
             if self.schedule == "staggered":
                 self._ev_op.record()
+        if self.schedule == "staggered":
+            self._join()
 
     def step(self):
         """One generation of C children (ga.cpp:543-585), enqueued on the island's
         stream(s): the whole batch, or (staggered) each sub-batch in turn."""
         if self.schedule == "staggered":
+            self._fork()
             for j in range(self.parts):
                 self._part_step(j)
+            self._join()
             self.generation += 1
             return
         with self._on_stream():
@@ -363,8 +398,10 @@ class Island(Members):
         import torch
         if self.schedule != "staggered":
             return
+        self._fork()
         while self._pending:
             self._replace_oldest()
+        self._join()
         with self._on_stream():
             torch.cuda.current_stream().wait_event(self._ev_op)
 
