@@ -220,8 +220,15 @@ def verify_shard(inst, slot, room, out, rows: int = 256) -> dict:
     s_np, r_np = slot[ti].cpu().numpy(), room[ti].cpu().numpy()
     got = [o[ti].cpu().numpy() for o in out]
     exp = split_rows(oracle().problem(inst).eval, (s_np, r_np), threads=max(1, host_threads() // 2))
-    ok = all(np.array_equal(g, e) for g, e in zip(got, exp))
-    return {"rows_checked": int(idx.size), "matches_oracle": bool(ok)}
+    names = ("hcv", "scv", "feasible", "penalty")
+    bad = {n: int((g != e).sum()) for n, g, e in zip(names, got, exp) if not np.array_equal(g, e)}
+    rec = {"rows_checked": int(idx.size), "matches_oracle": not bad}
+    if bad:                                   # enough to tell a wrong kernel from a wrong read
+        rows = np.nonzero(np.any([g != e for g, e in zip(got, exp)], axis=0))[0]
+        k = int(rows[0])
+        rec["mismatch"] = {"fields": bad, "rows": int(rows.size), "first_row": int(idx[k]),
+                           "gpu": [int(g[k]) for g in got], "oracle": [int(e[k]) for e in exp]}
+    return rec
 
 
 def rank_record(rank: int, dev, kernel_ms: float, wall: float, P: int, first: int, check: dict) -> dict:
@@ -242,7 +249,7 @@ def merge_ranks(records: list, backend: str, world: int) -> dict:
     return {"world": world, "backend": backend, "ranks_verified": sum(1 for r in records if r["matches_oracle"]),
             "rows_checked": sum(r["rows_checked"] for r in records), "distinct_devices": len(locs),
             "devices": [{k: r[k] for k in ("rank", "device", "pci", "uuid", "kernel_ms", "rows_checked",
-                                           "matches_oracle")} for r in records]}
+                                           "matches_oracle", "mismatch") if k in r} for r in records]}
 
 
 def main():

@@ -90,3 +90,6 @@ def test_rank_verification_gloo_world2():
     assert m["world"] == 2 and m["backend"] == "gloo" and m["distinct_devices"] == 2
     assert m["ranks_verified"] == 1 and m["rows_checked"] == 512
     assert [d["matches_oracle"] for d in m["devices"]] == [True, False]
+    bad = m["devices"][1]["mismatch"]
+    assert bad["fields"] == {"scv": 1} and bad["rows"] == 1 and bad["first_row"] == 599
+    assert bad["gpu"][1] == bad["oracle"][1] + 1 and "mismatch" not in m["devices"][0]

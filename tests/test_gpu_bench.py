@@ -91,7 +91,7 @@ def _assert_ranks(d, world, backend):
     reported the device it bound (gloo rehearsal: both ranks share the GPU)."""
     rk = d["ranks"]
     assert rk["world"] == world == d["n_gpus"] and rk["backend"] == backend
-    assert rk["ranks_verified"] == world and rk["rows_checked"] >= 256 * world
+    assert rk["ranks_verified"] == world and rk["rows_checked"] >= 256 * world, rk
     pairs = {(x["rank"], x["device"]) for x in rk["devices"]}
     assert len(pairs) == world and sorted(r for r, _ in pairs) == list(range(world))
     assert all(x["matches_oracle"] and x["kernel_ms"] > 0 and x["pci"] for x in rk["devices"])

@@ -126,6 +126,45 @@ def test_local_search_wide_rooms_crowded_slots_redo(orc, dims):
     assert dp.status() == 0
 
 
+@pytest.mark.parametrize("dims", [(1000, 40, 6, 300), (1000, 17, 5, 300), (1000, 16, 5, 300), (600, 10, 4, 200)],
+                         ids=["E1000R40", "E1000R17", "E1000R16", "E600R10"])
+def test_assign_rooms_slot_shapes_vs_oracle(orc, dims):
+    """tt_assign_rooms and tt_mutation on rows built to hit every matcher path:
+    the wave matcher (slots of 1-64 events), the lane-serial fallback (65-256
+    events; at R > 16 two such slots of one individual, an even and an odd one,
+    so both waves of the wide kernel take it at once), the register lanes of a
+    whole row at R <= 16 (<= 32 events) beside the wave (33-64), empty slots.
+    Rooms and mutated rows against the oracle, device status clean."""
+    inst = _inst(*dims, seed=123, att=(2, 8))
+    dp = native.DeviceProblem(inst)
+    o = orc.problem(inst)
+    E, P = inst.E, 48
+    rng = np.random.default_rng(17)
+    s0 = rng.integers(0, 45, size=(P, E), dtype=np.uint8)
+    for k in range(P):
+        kind = k % 4
+        ev = rng.permutation(E)
+        if kind == 0:                                   # two crowded slots, even and odd
+            a, b = 2 * int(rng.integers(0, 22)), 2 * int(rng.integers(0, 22)) + 1
+            s0[k, ev[:int(rng.integers(65, 257))]] = a
+            s0[k, ev[300:300 + int(rng.integers(65, 257))]] = b
+        elif kind == 1:                                 # slots of exactly 32, 33, 64 events; slot 44 empty
+            s0[k][s0[k] == 44] = 0
+            for t, n in ((3, 32), (4, 33), (5, 64)):
+                s0[k][s0[k] == t] = 6
+                s0[k, ev[100 * t:100 * t + n]] = t
+        elif kind == 2:                                 # few slots of ~40-70 events
+            s0[k] = rng.integers(0, max(1, E // 50), size=E).astype(np.uint8)
+    r0 = o.assign_rooms(s0)
+    assert np.array_equal(host(dp.assign_rooms(dev(s0))), r0)
+    ms = ttga.population_seeds(9400, P)
+    mslot, mroom, mrng = o.mutation(s0, r0, ms)
+    gs, gr, gg = dev(s0), dev(r0), dev(ms)
+    dp.mutation(gs, gr, gg)
+    assert np.array_equal(host(gs), mslot) and np.array_equal(host(gr), mroom) and np.array_equal(host(gg), mrng)
+    assert dp.status() == 0
+
+
 @pytest.mark.parametrize("dims", [(449, 24, 5, 220), (1000, 64, 6, 300)], ids=["E449R24", "E1000R64"])
 def test_variation_wide_rooms_vs_oracle(orc, dims):
     """RandomInitialSolution, crossover and mutation (Solution.cpp:48-61,

@@ -360,6 +360,11 @@ __device__ __forceinline__ void scv_terms(LsState& S, int e, bool nb, int& es, i
     LSP_ADD(S, kPfScv, t0);
 }
 
+// TT_LS_DISC_ALL: the room stage's discovering-room ballot over all room lanes,
+// masked by the uniform M afterwards (no per-lane M test).
+#ifndef TT_LS_DISC_ALL
+#define TT_LS_DISC_ALL 1
+#endif
 // TT_LS_WLT: the matcher's room transpose by v_writelane instead of a
 // compare-and-select per room.
 #ifndef TT_LS_WLT
@@ -434,7 +439,11 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
             const uint64_t freef = fr & ~rmatched;
             const uint64_t M = fr & (freef ? (freef & (0ull - freef)) - 1ull : ~0ull);
             const uint64_t plr = ((uint64_t)plr_hi << 32) | plr_lo;
+#if TT_LS_DISC_ALL
+            const uint64_t disc = ballot((plr & ~sr) != 0ull) & M;      // M is uniform: mask after the ballot
+#else
             const uint64_t disc = ballot(((M >> lane) & 1ull) && (plr & ~sr) != 0ull);
+#endif
             LSP_CNT(S, kPfMatchSteps);
             if (!disc) {                                   // the walk reaches the lowest free room
                 if (freef) sink = __builtin_ctzll(freef);

@@ -40,17 +40,19 @@ constexpr int kWaveSlots = 8;    // touched slots up to which every slot goes to
 //    rooms, room owners and dads, for one slot per lane;
 //  * R > 16 ("wide", TT_ROOMS_WAVE): the wave matcher keeps its state in
 //    registers and reads the possible rooms from the problem (L2-resident), so
-//    the scratch holds the row, its buckets and one crowded slot's state for
-//    the lane-serial fallback: 4E + 2.4 KB instead of 14E + 90R (syn: 11 KB
-//    instead of 30 KB, 14 instead of 5 waves per CU).
+//    the scratch holds the row, its buckets and, per wave, one crowded slot's
+//    state for the lane-serial fallback: 4E + 2.4 KB per wave instead of
+//    14E + 90R (syn: 11 KB for one wave, 13.8 KB for two, instead of 30 KB);
+//    in assign_rooms_kernel kWideWaves waves share an individual and split its
+//    slots, so at syn a CU holds 22 waves instead of 5.
 struct MatchScratch {
     uint8_t* sl;        // [E]     slot of each event
     uint8_t* rr;        // [E]     room of each event (output row)
     uint16_t* bev;      // [E]     events bucketed by slot, ascending inside a slot
-    uint8_t* mr;        // [E]     matched room per bucket position (kNone)   wide: [256], one slot
-    uint64_t* pl;       // [E]     possible-room mask per bucket position    wide: [256], one slot
-    uint8_t* rm;        // [45*R]  event (bucket-local index) matched to each room   wide: [R]
-    uint8_t* dr;        // [45*R]  dad (bucket-local event) of each room in the search   wide: [R]
+    uint8_t* mr;        // [E]     matched room per bucket position (kNone)   wide: [waves][256], one slot
+    uint64_t* pl;       // [E]     possible-room mask per bucket position    wide: [waves][256], one slot
+    uint8_t* rm;        // [45*R]  event (bucket-local index) matched to each room   wide: [waves][R]
+    uint8_t* dr;        // [45*R]  dad (bucket-local event) of each room in the search   wide: [waves][R]
     int32_t* bstart;    // [46]    bucket offsets
     uint32_t* tmp;      // [64]
     uint32_t* flags;    // [4]
@@ -59,11 +61,14 @@ struct MatchScratch {
 };
 
 __host__ __device__ inline bool match_wide(int R) { return TT_ROOMS_WAVE && R > 16; }
+constexpr int kWideWaves = 2;    // waves per individual in assign_rooms_kernel, wide layout
+static_assert(kWideWaves == 2, "assign_touched splits the slots into even and odd");
 
-__host__ __device__ inline size_t match_scratch_bytes(int E, int R) {
+// nw: waves sharing the individual (wide layout: one crowded slot's state each)
+__host__ __device__ inline size_t match_scratch_bytes(int E, int R, int nw = 1) {
     const bool wide = match_wide(R);
-    const size_t nb = wide ? (size_t)kMaxSlotEvents : (size_t)E;     // bucket positions with state
-    const size_t nr = wide ? (size_t)R : (size_t)kSlots * R;
+    const size_t nb = wide ? (size_t)nw * kMaxSlotEvents : (size_t)E;   // bucket positions with state
+    const size_t nr = wide ? (size_t)nw * R : (size_t)kSlots * R;
     size_t b = 0;
     b += (size_t)E;                          // sl
     b += (size_t)E;                          // rr
@@ -80,11 +85,11 @@ __host__ __device__ inline size_t match_scratch_bytes(int E, int R) {
     return (b + 15) & ~(size_t)15;
 }
 
-__device__ inline MatchScratch carve_match_scratch(uint8_t* base, int E, int R) {
+__device__ inline MatchScratch carve_match_scratch(uint8_t* base, int E, int R, int nw = 1) {
     MatchScratch m;
     m.wide = match_wide(R);
-    const size_t nb = m.wide ? (size_t)kMaxSlotEvents : (size_t)E;
-    const size_t nr = m.wide ? (size_t)R : (size_t)kSlots * R;
+    const size_t nb = m.wide ? (size_t)nw * kMaxSlotEvents : (size_t)E;
+    const size_t nr = m.wide ? (size_t)nw * R : (size_t)kSlots * R;
     size_t b = 0;
     m.sl = base + b; b += E;
     m.rr = base + b; b += E;
@@ -116,36 +121,39 @@ __device__ __forceinline__ int wave_inclusive_scan(int v, int lane) {
 // Bucket the events by slot, ascending event index inside each bucket
 // (the order of timeslot_events lists, which are always kept sorted).
 // All 64 lanes of the wave call this; sl[] must be filled.
-__device__ inline void build_buckets(const DevProblem& pb, MatchScratch& m, int lane) {
+// act: this wave does the work (a workgroup of several waves: the first; the
+// others only meet the barriers).
+__device__ inline void build_buckets(const DevProblem& pb, MatchScratch& m, int lane, bool act = true) {
     const int E = pb.E;
-    m.tmp[lane] = 0u;
+    if (act) m.tmp[lane] = 0u;
     __syncthreads();
-    for (int e = lane; e < E; e += 64) {
-        const int s = m.sl[e];
-        if (s < kSlots) atomicAdd(&m.tmp[s], 1u);
-    }
+    if (act)
+        for (int e = lane; e < E; e += 64) {
+            const int s = m.sl[e];
+            if (s < kSlots) atomicAdd(&m.tmp[s], 1u);
+        }
     __syncthreads();
     const int c = lane < kSlots ? (int)m.tmp[lane] : 0;
     const int incl = wave_inclusive_scan(c, lane);
     const int start = incl - c;
-    if (lane < kSlots) m.bstart[lane] = start;
-    if (lane == kSlots - 1) m.bstart[kSlots] = incl;
+    if (act && lane < kSlots) m.bstart[lane] = start;
+    if (act && lane == kSlots - 1) m.bstart[kSlots] = incl;
 #if TT_BUCKETS_CHUNK
     // stable fill, 64 events at a time: each event sets its lane bit in its slot's
     // chunk mask; its place is the slot's running count plus the lower lanes of the
     // mask (ascending event order inside a bucket, as the lane walk below)
-    m.cm[lane] = 0ull;
+    if (act) m.cm[lane] = 0ull;
     int cur = start;                                  // lane t < 45: slot t's next position
     __syncthreads();
     for (int c0 = 0; c0 < E; c0 += 64) {
         const int e = c0 + lane;
-        const int s = e < E ? m.sl[e] : 0xFF;
+        const int s = act && e < E ? m.sl[e] : 0xFF;
         if (s < kSlots) atomicOr((unsigned long long*)&m.cm[s], 1ull << lane);
         const int base = __shfl(cur, s < kSlots ? s : 0, 64);       // every lane takes part
         __syncthreads();
         if (s < kSlots) m.bev[base + __popcll(m.cm[s] & ((1ull << lane) - 1ull))] = (uint16_t)e;
         __syncthreads();
-        if (lane < kSlots) {
+        if (act && lane < kSlots) {
             cur += __popcll(m.cm[lane]);
             m.cm[lane] = 0ull;
         }
@@ -165,9 +173,10 @@ __device__ inline void build_buckets(const DevProblem& pb, MatchScratch& m, int 
     }
     for (; e < E; ++e)
         if (m.sl[e] == me) m.bev[pos++] = (uint16_t)e;
+    static_assert(TT_BUCKETS_CHUNK, "the lane walk has no act flag");
 #endif
     __syncthreads();
-    if (m.wide) return;                                // the wave matcher reads pb.poss itself
+    if (m.wide || !act) return;                        // wide: the wave matcher reads pb.poss itself
     const int nb = m.bstart[kSlots];
     for (int b0 = 0; b0 < nb; b0 += 512) {            // eight gathers in flight per block
         uint64_t v[8];
@@ -430,7 +439,8 @@ __device__ __forceinline__ uint32_t wave_match_slot(int R, int N, uint64_t pl, i
             const uint64_t freef = fr & ~rmatched;
             const uint64_t M = fr & (freef ? (freef & (0ull - freef)) - 1ull : ~0ull);
             const uint64_t plr = ((uint64_t)plr_hi << 32) | plr_lo;
-            const uint64_t disc = ballot(((M >> lane) & 1ull) && (plr & ~sr) != 0ull);
+            // M is uniform: one ballot over every room lane, then M's lanes kept
+            const uint64_t disc = ballot((plr & ~sr) != 0ull) & M;
             if (!disc) {
                 if (freef) sink = __builtin_ctzll(freef);
                 break;
@@ -482,10 +492,13 @@ __device__ __forceinline__ uint32_t wave_match_slot(int R, int N, uint64_t pl, i
 // Re-assign rooms for every slot t with bit t of `touched` set and a
 // non-empty bucket. m.sl and m.rr hold the individual's row; rooms of
 // untouched slots in m.rr are left as they are. Buckets must be built.
-__device__ inline void assign_touched(const DevProblem& pb, MatchScratch& m, uint64_t touched, int lane) {
+// wave w of nw: the slots t with t % nw == w (wide layout only).
+__device__ inline void assign_touched(const DevProblem& pb, MatchScratch& m, uint64_t touched, int lane,
+                                      int w = 0, int nw = 1) {
 #if TT_ROOMS_WAVE
     const int R = pb.R;
     touched &= (1ull << kSlots) - 1ull;
+    if (nw == 2) touched &= w ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
     if (!m.wide && __popcll(touched) > kWaveSlots) {
         // a whole row on a small instance: slots of <= 32 events one per lane, in
         // registers, all at once; the crowded ones go to the wave below
@@ -523,15 +536,15 @@ __device__ inline void assign_touched(const DevProblem& pb, MatchScratch& m, uin
             const uint32_t r = wave_match_slot(R, Nc, plc, lane);
             if (lane < Nc) m.rr[evc] = (uint8_t)r;
         } else if (Nc <= kMaxSlotEvents) {
-            uint64_t* spl = m.wide ? m.pl : m.pl + bc;                     // the wide layout: one slot's state
-            uint8_t* smr = m.wide ? m.mr : m.mr + bc;
-            uint8_t* srm = m.wide ? m.rm : m.rm + tc * R;
-            uint8_t* sdr = m.wide ? m.dr : m.dr + tc * R;
-            if (m.wide)
-                for (int i = lane; i < Nc; i += 64) spl[i] = pb.poss[m.bev[bc + i]];
-            __syncthreads();
-            if (lane == 0) match_slot<4>(R, m.bev + bc, spl, Nc, smr, srm, sdr, m.rr);
-            __syncthreads();
+            if (lane == 0) {                    // rare: one lane, no barrier (the waves' slots differ)
+                uint64_t* spl = m.wide ? m.pl + w * kMaxSlotEvents : m.pl + bc;   // wide: the wave's slot state
+                uint8_t* smr = m.wide ? m.mr + w * kMaxSlotEvents : m.mr + bc;
+                uint8_t* srm = m.wide ? m.rm + w * R : m.rm + tc * R;
+                uint8_t* sdr = m.wide ? m.dr + w * R : m.dr + tc * R;
+                if (m.wide)
+                    for (int i = 0; i < Nc; ++i) spl[i] = pb.poss[m.bev[bc + i]];
+                match_slot<4>(R, m.bev + bc, spl, Nc, smr, srm, sdr, m.rr);
+            }
         } else {
             for (int i = lane; i < Nc; i += 64) m.rr[m.bev[bc + i]] = 0xFF;
             if (lane == 0) atomicOr(pb.status, 1);

@@ -37,22 +37,28 @@ __device__ inline void store_row(uint8_t* dst, const uint8_t* src, int E, int la
 }
 
 // ---------------------------------------------------------------- assign
-__global__ __launch_bounds__(64) void assign_rooms_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
-                                                          uint8_t* __restrict__ room, int P,
-                                                          const uint8_t* __restrict__ mask, uint8_t bit) {
+// One individual per workgroup of 64 threads, or (wide layout, R > 16) of
+// kWideWaves waves: the first loads the row and builds the buckets, then the
+// waves match alternate slots (their searches are long; a shared individual
+// halves the LDS per wave, so twice as many waves hide each other's latency).
+__global__ __launch_bounds__(64 * kWideWaves) void assign_rooms_kernel(DevProblem pb, const uint8_t* __restrict__ slot,
+                                                                       uint8_t* __restrict__ room, int P,
+                                                                       const uint8_t* __restrict__ mask, uint8_t bit) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int E = pb.E, lane = threadIdx.x;
+    const int E = pb.E, lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const long p = blockIdx.x;
     if (mask && !(mask[p] & bit)) return;
-    MatchScratch m = carve_match_scratch(lds, E, pb.R);
-    load_row(m.sl, slot + p * E, E, lane);
-    for (int e = lane; e < E; e += 64) m.rr[e] = 0xFF;   // events with an invalid slot stay 255
+    MatchScratch m = carve_match_scratch(lds, E, pb.R, nw);
+    if (w == 0) {
+        load_row(m.sl, slot + p * E, E, lane);
+        for (int e = lane; e < E; e += 64) m.rr[e] = 0xFF;   // events with an invalid slot stay 255
+    }
     __syncthreads();
-    build_buckets(pb, m, lane);
+    build_buckets(pb, m, lane, w == 0);
 #if TT_ROOMS_ABL != 1                                    // profiling builds only: buckets alone
-    assign_touched(pb, m, ~0ull, lane);
+    assign_touched(pb, m, ~0ull, lane, w, nw);
 #endif
-    store_row(room + p * E, m.rr, E, lane);
+    if (w == 0) store_row(room + p * E, m.rr, E, lane);
 }
 
 // ---------------------------------------------------------------- lane-per-individual slot generators
@@ -175,9 +181,11 @@ static int tile_stride(int E) { return (E + 3) & ~3; }
 
 int launch_assign_masked(const tt_problem* p, const uint8_t* slot, uint8_t* room, int P, const uint8_t* mask,
                          uint8_t bit, hipStream_t st) {
-    const size_t lds = match_scratch_bytes(p->E, p->R);
+    const int nw = match_wide(p->R) ? kWideWaves : 1;
+    const size_t lds = match_scratch_bytes(p->E, p->R, nw);
     if (lds > 160 * 1024) { set_error("instance too large for the matcher"); return TT_ERR_LIMIT; }
-    hipLaunchKernelGGL(assign_rooms_kernel, dim3(P), dim3(64), lds, st, p->dev, slot, room, P, mask, bit);
+    const int threads = 64 * nw;
+    hipLaunchKernelGGL(assign_rooms_kernel, dim3(P), dim3(threads), lds, st, p->dev, slot, room, P, mask, bit);
     return check_hip(hipGetLastError(), "assign_rooms launch");
 }
 
