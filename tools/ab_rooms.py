@@ -1,5 +1,6 @@
 """Same-box A/B timing of the room-assignment and mutation kernels (profiling
-only; tools/ab_build.sh makes the libraries): tt_assign_rooms and tt_mutation
+only; tools/ab_build.sh makes the libraries, "tree" is the in-tree one):
+tt_assign_rooms and tt_mutation
 on P rows of random slots of an instance, every library's output compared with
 the first, HIP-event medians over rounds.
 
@@ -22,7 +23,8 @@ names = sys.argv[3:]
 inst = ttga.config_instance(cfg)
 probs = {}
 for name in names:
-    lib = native.load(REPO / "ab_libs" / f"libttga_{name}.so")
+    lib = native.load(REPO / "timetabling-ga-mpi-openmp_amd" / "libttga.so" if name == "tree"
+                      else REPO / "ab_libs" / f"libttga_{name}.so")
     saved, native._lib = native._lib, lib
     probs[name] = native.DeviceProblem(inst)
     native._lib = saved

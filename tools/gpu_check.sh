@@ -71,7 +71,7 @@ for s in $STEPS; do
     stagl) for c in ${STAGCFGS:-comp20 comp15}; do for l in on off; do run ga8k_${c}_stag_lpt$l 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --schedule staggered --lpt $l; done; run ga8k_${c}_batch 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0; done ;;
     lsevaltests) run pytest_lseval 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_ga.py tests/test_gpu_configs.py tests/test_gpu_baseline_configs.py tests/test_gpu_wide_rooms.py -m gpu -q --timeout 300 --timeout-method thread ;;
     abrooms) for c in ${ROOMCFGS:-syn:65536 comp01:65536 med:65536 lg:65536}; do run ab_rooms_${c%%:*} 300 python -u tools/ab_rooms.py ${c%%:*} ${c##*:} ${LIBS:-rw0 rw1}; done ;;
-    roomroof) run rooms_roofline 900 python -u tools/rooms_roofline.py ${ROOMROOF:---config syn:65536 --config comp01:65536} --lib ${ROOMLIB:-rw3} --out "$OUT/rooms_roofline.jsonl" ;;
+    roomroof) run rooms_roofline 900 python -u tools/rooms_roofline.py ${ROOMROOF:---config syn:65536 --config comp01:65536} --lib ${ROOMLIB:-tree} --out "$OUT/rooms_roofline.jsonl" ;;
     benchtests) run pytest_bench 600 python -u -m pytest tests/test_gpu_bench.py -m gpu -v --timeout 300 --timeout-method thread ;;
     gatests) run pytest_ga 600 python -u -m pytest tests/test_gpu_ga.py -m gpu -v --timeout 300 --timeout-method thread ;;
     derive) run pytest_derive 400 python -u -m pytest tests/test_gpu_derive.py -m gpu -v --timeout 200 --timeout-method thread ;;

@@ -9,9 +9,11 @@ their rate against 8 TB/s, and from hardware counters (rocprofv3 --pmc, one
 process per pass, tools/ab_rooms.py as the workload, medians over its timed
 launches) the issue rate per SIMD-cycle against 1, VALU / SALU busy, the
 waves' wait share, instructions per individual and per slot, and the
-HBM traffic (FETCH_SIZE / WRITE_SIZE) against the algorithmic bytes.
+HBM traffic (FETCH_SIZE / WRITE_SIZE) against the algorithmic bytes; beside
+it assignRooms on the host cores (cpu_baseline: the reference's own objects,
+or at syn the oracle's restatement).
 
-    python tools/rooms_roofline.py [--config syn:65536 --config comp01:65536] [--lib rw3] [--out x.jsonl]
+    python tools/rooms_roofline.py [--config syn:65536 --config comp01:65536] [--lib tree] [--out x.jsonl]
 """
 import argparse
 import json
@@ -69,6 +71,29 @@ def timed(cfg: str, P: int, lib: str) -> dict:
     return json.loads(r.stdout[r.stdout.index("{"):])
 
 
+def cpu_leg(inst, rows: int) -> dict | None:
+    """assignRooms on `rows` random rows on the host cores: the reference's own
+    objects (oracle/_ref) where building its Problem is quick, else the
+    oracle's restatement (the reference parses syn's Problem for ~108 s)."""
+    import time
+
+    import numpy as np
+    sys.path.insert(0, str(REPO / "tests"))
+    from oracle_lib import host_threads, oracle, ref, split_rows
+    kind, lib = ("reference", ref()) if inst.E <= 1000 else ("port", None)
+    if lib is None:
+        kind, lib = "port", oracle()
+    if lib is None:
+        return None
+    h = lib.problem(inst)
+    s = np.random.default_rng(5).integers(0, 45, size=(rows, inst.E), dtype=np.uint8)
+    T = host_threads()
+    t0 = time.perf_counter()
+    split_rows(lambda x: (h.assign_rooms(x),), (s,), threads=T)
+    dt = time.perf_counter() - t0
+    return {"kind": kind, "cores": T, "rows": rows, "seconds": dt, "individuals_per_s": rows / dt}
+
+
 def derive(c: dict, E: int, P: int, ms: float) -> dict:
     cyc = c["cycles_insts"]
     alg = 2.0 * E * P                                   # slot row in, room row out
@@ -93,8 +118,9 @@ def derive(c: dict, E: int, P: int, ms: float) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", action="append", default=None, help="instance:P")
-    ap.add_argument("--lib", default="rw3", help="ab_libs/libttga_<lib>.so (tools/ab_build.sh)")
+    ap.add_argument("--lib", default="tree", help="tree (the in-tree library) or ab_libs/libttga_<lib>.so")
     ap.add_argument("--timeout", type=int, default=180)
+    ap.add_argument("--cpu-rows", type=int, default=0, help="rows of the CPU leg (0: 512 at syn, else 4096)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     sys.path.insert(0, str(REPO / "timetabling-ga-mpi-openmp_amd"))
@@ -107,6 +133,7 @@ def main():
         c = collect(cfg, P, a.lib, a.timeout)
         rec = {"config": cfg, "E": inst.E, "R": inst.R, "P": P, "lib": a.lib, "kernel": KERNEL,
                "mutation_ms": t["mutation"][a.lib], "line": derive(c, inst.E, P, t["assign"][a.lib]),
+               "cpu_baseline": cpu_leg(inst, a.cpu_rows or (512 if inst.E > 1000 else 4096)),
                "meta": c.pop("meta", {}), "raw": c}
         recs.append(rec)
         print(json.dumps(rec), flush=True)
