@@ -73,6 +73,7 @@ for s in $STEPS; do
     abrooms) for c in ${ROOMCFGS:-syn:65536 comp01:65536 med:65536 lg:65536}; do run ab_rooms_${c%%:*} 300 python -u tools/ab_rooms.py ${c%%:*} ${c##*:} ${LIBS:-rw0 rw1}; done ;;
     roomroof) run rooms_roofline 900 python -u tools/rooms_roofline.py ${ROOMROOF:---config syn:65536 --config comp01:65536} --lib ${ROOMLIB:-tree} --out "$OUT/rooms_roofline.jsonl" ;;
     benchtests) run pytest_bench 600 python -u -m pytest tests/test_gpu_bench.py -m gpu -v --timeout 300 --timeout-method thread ;;
+    gastagab) for i in 1 2; do for c in ${GACFGS:-comp15 comp16 comp01}; do for sch in ${STAGSCH:-staggered}; do for l in $LIBS; do run ga8k_${c}_${sch}_${l}_$i 300 python -u tools/bench_ga.py --config $c --pop 65536 --children 8192 --steps 1000 --warm-gens 96 --warm-feasible 0.6 --gens 25 --min-seconds 1.0 --cpu-sample 0 --schedule $sch --lib ab_libs/libttga_$l.so; done; done; done; done ;;
     gatests) run pytest_ga 600 python -u -m pytest tests/test_gpu_ga.py -m gpu -v --timeout 300 --timeout-method thread ;;
     derive) run pytest_derive 400 python -u -m pytest tests/test_gpu_derive.py -m gpu -v --timeout 200 --timeout-method thread ;;
     newtests) run pytest_new 600 python -u -m pytest tests/test_gpu_derive.py tests/test_gpu_ga.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread -k "derive or derived or permutation or redo" ;;
