@@ -423,7 +423,7 @@ __device__ __forceinline__ void match_task_wave(LsState& S, int k, int N, int ev
     for (;;) {
         // stage 1 (closed form): expand all unmatched events, ascending
         const uint64_t cand = eor & unm;
-        uint64_t sr = ballot(lane < R && cand != 0ull), fr = sr;
+        uint64_t sr = ballot(cand != 0ull), fr = sr;          // eor is zero on lanes >= R (no room bit there)
         if (cand) dr = (uint32_t)__builtin_ctzll(cand);
         // stage 2: fringe rooms ascending; a matched room's event is expanded at
         // once. Each room enters the fringe once and each matched event is
