@@ -42,9 +42,10 @@ constexpr int kWaveSlots = 8;    // touched slots up to which every slot goes to
 //    registers and reads the possible rooms from the problem (L2-resident), so
 //    the scratch holds the row, its buckets and, per wave, one crowded slot's
 //    state for the lane-serial fallback: 4E + 2.4 KB per wave instead of
-//    14E + 90R (syn: 11 KB for one wave, 13.8 KB for two, instead of 30 KB);
-//    in assign_rooms_kernel kWideWaves waves share an individual and split its
-//    slots, so at syn a CU holds 22 waves instead of 5.
+//    14E + 90R (syn: 11 KB for one wave, 18.5 KB for four, instead of 30 KB);
+//    in assign_rooms_kernel kWideWaves waves share an individual and take its
+//    slots t with t % kWideWaves == wave (syn, 65,536 rows: one wave 23.7 ms,
+//    two 20.0, three 19.4, four 18.8; profiles/r06_ae_ab_rooms_waves.jsonl).
 struct MatchScratch {
     uint8_t* sl;        // [E]     slot of each event
     uint8_t* rr;        // [E]     room of each event (output row)
@@ -61,8 +62,10 @@ struct MatchScratch {
 };
 
 __host__ __device__ inline bool match_wide(int R) { return TT_ROOMS_WAVE && R > 16; }
-constexpr int kWideWaves = 2;    // waves per individual in assign_rooms_kernel, wide layout
-static_assert(kWideWaves == 2, "assign_touched splits the slots into even and odd");
+#ifndef TT_WIDE_WAVES
+#define TT_WIDE_WAVES 4
+#endif
+constexpr int kWideWaves = TT_WIDE_WAVES;    // waves per individual in assign_rooms_kernel, wide layout
 
 // nw: waves sharing the individual (wide layout: one crowded slot's state each)
 __host__ __device__ inline size_t match_scratch_bytes(int E, int R, int nw = 1) {
@@ -498,7 +501,11 @@ __device__ inline void assign_touched(const DevProblem& pb, MatchScratch& m, uin
 #if TT_ROOMS_WAVE
     const int R = pb.R;
     touched &= (1ull << kSlots) - 1ull;
-    if (nw == 2) touched &= w ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
+    if (nw > 1) {                                       // this wave's slots: t % nw == w
+        uint64_t wm = 0;
+        for (int t = w; t < kSlots; t += nw) wm |= 1ull << t;
+        touched &= wm;
+    }
     if (!m.wide && __popcll(touched) > kWaveSlots) {
         // a whole row on a small instance: slots of <= 32 events one per lane, in
         // registers, all at once; the crowded ones go to the wave below
