@@ -259,6 +259,34 @@ __device__ __forceinline__ int corr_in_set(LsState& S, int e, const uint64_t* se
     return c - self;
 }
 
+// TT_LS_ROWB: a lane's own correlation row (corr64[e], EW words in L2) against an
+// LDS word set, loaded 8 words at a time with all 8 loads in flight before the
+// first is used -- the plain word loop waited out one L2 round trip per word
+// (EW of them per row; 49 per whole-population pass at E = 400).
+#ifndef TT_LS_ROWB
+#define TT_LS_ROWB 1
+#endif
+// sum over w < EW of popcount(row[w] & set[w]) minus the row's own bit e
+__device__ __forceinline__ int row_pop_in(const uint64_t* __restrict__ row, const uint64_t* set, int EW, int e) {
+    int c = 0;
+#if TT_LS_ROWB
+    for (int w0 = 0; w0 < EW; w0 += 8) {
+        uint64_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = w0 + k < EW ? row[w0 + k] : 0ull;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            c += __popcll(x[k] & (w0 + k < EW ? set[w0 + k] : 0ull));
+            if (w0 + k == (e >> 6)) c -= (int)((x[k] >> (e & 63)) & 1ull);
+        }
+    }
+#else
+    for (int w = 0; w < EW; ++w) c += __popcll(row[w] & set[w]);
+    c -= (int)((row[e >> 6] >> (e & 63)) & 1ull);
+#endif
+    return c;
+}
+
 // eventAffectedHcv(e) (Solution.cpp:194-215) in the current state
 __device__ __forceinline__ int eah_cur(LsState& S, int e) {
     const int t = S.sl[e];
@@ -894,9 +922,7 @@ __device__ __forceinline__ bool feasible_now(LsState& S) {
         const int e = 64 * k + S.lane;
         if (e < S.E) {
             const int t = S.sl[e];
-            int c = 0;
-            for (int w = 0; w < S.EW; ++w) c += __popcll(S.pb.corr64[(size_t)e * S.EW + w] & S.B[(size_t)t * S.EW + w]);
-            c -= (int)((S.pb.corr64[(size_t)e * S.EW + (e >> 6)] >> (e & 63)) & 1ull);
+            const int c = row_pop_in(S.pb.corr64 + (size_t)e * S.EW, S.B + (size_t)t * S.EW, S.EW, e);
             h += c;   // every correlated same-slot pair is counted twice, only zero matters
             h += (int)(((S.pb.poss[e] >> S.rr[e]) & 1ull) ^ 1ull);
         }
@@ -1302,10 +1328,8 @@ __device__ __forceinline__ uint64_t refresh_hot(LsState& S, uint64_t hot, bool a
             const int t = S.sl[e];
             upd = all || (S.nts > 0 && t == S.ts[0]) || (S.nts > 1 && t == S.ts[1]) || (S.nts > 2 && t == S.ts[2]);
             if (upd) {
-                int c = (int)S.hist[t * R + S.rr[e]] - 1;
-                const uint64_t* row = S.pb.corr64 + (size_t)e * EW;
-                for (int w = 0; w < EW; ++w) c += __popcll(row[w] & S.B[(size_t)t * EW + w]);
-                c -= (int)((row[e >> 6] >> (e & 63)) & 1ull);
+                const int c = (int)S.hist[t * R + S.rr[e]] - 1 +
+                              row_pop_in(S.pb.corr64 + (size_t)e * EW, S.B + (size_t)t * EW, EW, e);
                 h = c > 0;
             }
         }
@@ -1363,8 +1387,7 @@ __device__ __forceinline__ void ls_eval(LsState& S, long p, const LsEvalOut& out
     int cp = 0;                                            // 2 x correlated pairs
     for (int e = lane; e < E; e += 64) {
         const int t = S.sl[e], r = S.rr[e];
-        for (int w = 0; w < EW; ++w) cp += __popcll(pb.corr64[(size_t)e * EW + w] & S.B[(size_t)t * EW + w]);
-        cp -= (int)((pb.corr64[(size_t)e * EW + (e >> 6)] >> (e & 63)) & 1ull);   // corr(e, e): e has a student
+        cp += row_pop_in(pb.corr64 + (size_t)e * EW, S.B + (size_t)t * EW, EW, e);   // minus corr(e, e): e has a student
         h += (int)(((pb.poss[e] >> r) & 1ull) ^ 1ull);
         if ((kLastSlotMask >> t) & 1ull) sc += pb.sn[e];
     }
